@@ -1,0 +1,103 @@
+// Common device-side helpers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "bdx_lattice.h"
+
+#define BDX_CHECK(expr)                                                     \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess) return static_cast<int>(_e);                      \
+  } while (0)
+
+constexpr int kMaxNd = 8;
+constexpr int kMaxNq = 9;
+
+// 1D operator tables, passed by value as a kernel argument (< 1.5 KiB).
+template <typename T>
+struct OpTables {
+  T phi0[kMaxNq * kMaxNd];    // nq x nd, interpolation to quadrature points
+  T dphi1[kMaxNq * kMaxNq];   // nq x nq, derivative on quadrature nodes
+  T wts[kMaxNq];              // 1D quadrature weights
+  T qpts[kMaxNq];             // 1D quadrature points on [0, 1]
+  int identity;               // phi0 == I (collocated: qmode 0 + GLL)
+};
+
+template <typename T>
+inline OpTables<T> make_op_tables(int nd, int nq, const double* phi0,
+                                  const double* dphi1, const double* wts,
+                                  const double* qpts, int identity) {
+  OpTables<T> t{};
+  for (int q = 0; q < nq; ++q) {
+    for (int i = 0; i < nd; ++i) t.phi0[q * nd + i] = static_cast<T>(phi0[q * nd + i]);
+    for (int j = 0; j < nq; ++j) t.dphi1[q * nq + j] = static_cast<T>(dphi1[q * nq + j]);
+    t.wts[q] = static_cast<T>(wts[q]);
+    t.qpts[q] = static_cast<T>(qpts[q]);
+  }
+  t.identity = identity;
+  return t;
+}
+
+// Trilinear geometry at reference point (s, t, u) of the cell with vertices
+// X (v = 4a+2b+c): returns det J and writes G = w adj(J) adj(J)^T / det J.
+template <typename T>
+__device__ __forceinline__ T geometry_G(const T (*X)[3], T s, T t, T u, T w,
+                                        T G[6]) {
+  T J[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    // d x_i / d s = sum over the 4 edges in s of (x_hi - x_lo) * bilinear(t, u)
+    const T e00 = X[4][i] - X[0][i], e01 = X[5][i] - X[1][i];
+    const T e10 = X[6][i] - X[2][i], e11 = X[7][i] - X[3][i];
+    J[i][0] = (1 - t) * ((1 - u) * e00 + u * e01) + t * ((1 - u) * e10 + u * e11);
+    const T f00 = X[2][i] - X[0][i], f01 = X[3][i] - X[1][i];
+    const T f10 = X[6][i] - X[4][i], f11 = X[7][i] - X[5][i];
+    J[i][1] = (1 - s) * ((1 - u) * f00 + u * f01) + s * ((1 - u) * f10 + u * f11);
+    const T g00 = X[1][i] - X[0][i], g01 = X[3][i] - X[2][i];
+    const T g10 = X[5][i] - X[4][i], g11 = X[7][i] - X[6][i];
+    J[i][2] = (1 - s) * ((1 - t) * g00 + t * g01) + s * ((1 - t) * g10 + t * g11);
+  }
+  const T K00 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+  const T K01 = J[0][2] * J[2][1] - J[0][1] * J[2][2];
+  const T K02 = J[0][1] * J[1][2] - J[0][2] * J[1][1];
+  const T K10 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+  const T K11 = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+  const T K12 = J[0][2] * J[1][0] - J[0][0] * J[1][2];
+  const T K20 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+  const T K21 = J[0][1] * J[2][0] - J[0][0] * J[2][1];
+  const T K22 = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+  const T det = J[0][0] * K00 + J[0][1] * K10 + J[0][2] * K20;
+  const T sc = w / det;
+  G[0] = (K00 * K00 + K01 * K01 + K02 * K02) * sc;
+  G[1] = (K10 * K00 + K11 * K01 + K12 * K02) * sc;
+  G[2] = (K20 * K00 + K21 * K01 + K22 * K02) * sc;
+  G[3] = (K10 * K10 + K11 * K11 + K12 * K12) * sc;
+  G[4] = (K20 * K10 + K21 * K11 + K22 * K12) * sc;
+  G[5] = (K20 * K20 + K21 * K21 + K22 * K22) * sc;
+  return det;
+}
+
+// Wave64 sum reduction via DPP-friendly shuffles.
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Block sum (blockDim.x multiple of 64, <= 1024); result valid in thread 0.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* lds /* >= 16 */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  T s = 0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int w = 0; w < nw; ++w) s += lds[w];
+  }
+  return s;
+}

@@ -1,0 +1,212 @@
+// Device BLAS-1, CG vector updates, halo pack/unpack (gfx950).
+//
+// Replaces the reference's Thrust calls (src/vector.hpp:151-292,
+// src/cg.hpp:21-79) and pack/unpack kernels (src/vector.hpp:31-62).
+// Differences by design:
+//   * every reduction is device-resident: per-block partials + one
+//     fixed-order final pass into a float64 scalar slot (deterministic, no
+//     host round trip); the all-reduce then runs on that device scalar;
+//   * the CG scalars (alpha, beta) are formed on the device from those slots;
+//   * x/r updates and the r.r reduction are one fused pass;
+//   * reductions and updates walk the owned sub-box of the local lattice
+//     one z-row per wave (rows are 128-byte aligned by the storage pitch).
+#include "bdx_common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+struct RowSpace {
+  int64_t L1, ld;       // storage strides
+  int64_t o0, o1, o2;   // owned extents
+};
+
+__device__ __forceinline__ int64_t row_base(const RowSpace& s, int64_t row) {
+  const int64_t i = row / s.o1, j = row - i * s.o1;
+  return (i * s.L1 + j) * s.ld;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+    dot_rows_kernel(RowSpace s, const T* __restrict__ a, const T* __restrict__ b,
+                    double* __restrict__ partials) {
+  __shared__ double lds[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nrows = s.o0 * s.o1;
+  double acc = 0.0;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < nrows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row_base(s, row);
+    for (int64_t k = lane; k < s.o2; k += 64)
+      acc += static_cast<double>(a[base + k]) * static_cast<double>(b[base + k]);
+  }
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+// Fixed-order sum of partials into out[slot] (single block).
+__global__ void __launch_bounds__(kBlock)
+    reduce_partials_kernel(const double* __restrict__ partials, int n,
+                           double* __restrict__ out, int slot) {
+  __shared__ double lds[16];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partials[i];
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) out[slot] = t;
+}
+
+// CG: alpha = s[rn] / s[pap];  x += alpha p;  r -= alpha y;  partial r.r
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+    cg_update_kernel(RowSpace s, T* __restrict__ x, T* __restrict__ r,
+                     const T* __restrict__ p, const T* __restrict__ y,
+                     const double* __restrict__ scal, int rn_slot, int pap_slot,
+                     double* __restrict__ partials) {
+  __shared__ double lds[16];
+  const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nrows = s.o0 * s.o1;
+  double acc = 0.0;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < nrows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row_base(s, row);
+    for (int64_t k = lane; k < s.o2; k += 64) {
+      const int64_t i = base + k;
+      x[i] = x[i] + alpha * p[i];
+      const T rn = r[i] - alpha * y[i];
+      r[i] = rn;
+      acc += static_cast<double>(rn) * static_cast<double>(rn);
+    }
+  }
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+// p = beta p + r with beta = s[num] / s[den] (owned rows).
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+    p_update_kernel(RowSpace s, T* __restrict__ p, const T* __restrict__ r,
+                    const double* __restrict__ scal, int num, int den) {
+  const T beta = static_cast<T>(scal[num] / scal[den]);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nrows = s.o0 * s.o1;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < nrows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row_base(s, row);
+    for (int64_t k = lane; k < s.o2; k += 64) p[base + k] = beta * p[base + k] + r[base + k];
+  }
+}
+
+// out = alpha x + y over owned rows (reference axpy, src/vector.hpp:228-240).
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+    axpy_kernel(RowSpace s, T* __restrict__ out, T alpha, const T* __restrict__ x,
+                const T* __restrict__ y) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nrows = s.o0 * s.o1;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < nrows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row_base(s, row);
+    for (int64_t k = lane; k < s.o2; k += 64) out[base + k] = alpha * x[base + k] + y[base + k];
+  }
+}
+
+// ------------------------------------------------------------- halo boxes
+// Box table in device memory: per box {lo0,lo1,lo2, e0,e1,e2, offset} (int64).
+constexpr int kBoxFields = 7;
+
+template <typename T, int MODE>  // 0 pack, 1 unpack (assign), 2 unpack (add)
+__global__ void __launch_bounds__(kBlock)
+    box_copy_kernel(T* __restrict__ vec, int64_t L1, int64_t ld,
+                    const int64_t* __restrict__ boxes, int nboxes, int64_t total,
+                    T* __restrict__ buf) {
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * kBlock) {
+    int b = 0;
+    while (b + 1 < nboxes && boxes[(b + 1) * kBoxFields + 6] <= t) ++b;
+    const int64_t* bx = boxes + b * kBoxFields;
+    const int64_t o = t - bx[6];
+    const int64_t e1 = bx[4], e2 = bx[5];
+    const int64_t k = o % e2, j = (o / e2) % e1, i = o / (e1 * e2);
+    const int64_t v = ((bx[0] + i) * L1 + (bx[1] + j)) * ld + (bx[2] + k);
+    if constexpr (MODE == 0)
+      buf[t] = vec[v];
+    else if constexpr (MODE == 1)
+      vec[v] = buf[t];
+    else
+      vec[v] += buf[t];
+  }
+}
+
+int grid_for_rows(int64_t nrows) {
+  const int64_t want = (nrows + kWaves - 1) / kWaves;
+  return static_cast<int>(want < 2048 ? (want > 0 ? want : 1) : 2048);
+}
+
+}  // namespace
+
+extern "C" {
+
+int bdx_hip_partials_size() { return 2048; }
+
+#define BDX_BLAS_API(T, SUF)                                                  \
+  int bdx_dot_##SUF(int64_t L1, int64_t ld, int64_t o0, int64_t o1, int64_t o2, \
+                    const T* a, const T* b, double* partials, double* out,    \
+                    int slot, hipStream_t st) {                               \
+    RowSpace s{L1, ld, o0, o1, o2};                                           \
+    const int g = grid_for_rows(o0 * o1);                                     \
+    dot_rows_kernel<T><<<g, kBlock, 0, st>>>(s, a, b, partials);              \
+    reduce_partials_kernel<<<1, kBlock, 0, st>>>(partials, g, out, slot);     \
+    return static_cast<int>(hipGetLastError());                               \
+  }                                                                           \
+  int bdx_cg_update_##SUF(int64_t L1, int64_t ld, int64_t o0, int64_t o1,     \
+                          int64_t o2, T* x, T* r, const T* p, const T* y,     \
+                          double* scal, int rn_slot, int pap_slot,            \
+                          int out_slot, double* partials, hipStream_t st) {   \
+    RowSpace s{L1, ld, o0, o1, o2};                                           \
+    const int g = grid_for_rows(o0 * o1);                                     \
+    cg_update_kernel<T><<<g, kBlock, 0, st>>>(s, x, r, p, y, scal, rn_slot,   \
+                                              pap_slot, partials);            \
+    reduce_partials_kernel<<<1, kBlock, 0, st>>>(partials, g, scal, out_slot); \
+    return static_cast<int>(hipGetLastError());                               \
+  }                                                                           \
+  int bdx_p_update_##SUF(int64_t L1, int64_t ld, int64_t o0, int64_t o1,      \
+                         int64_t o2, T* p, const T* r, const double* scal,    \
+                         int num, int den, hipStream_t st) {                  \
+    RowSpace s{L1, ld, o0, o1, o2};                                           \
+    p_update_kernel<T><<<grid_for_rows(o0 * o1), kBlock, 0, st>>>(s, p, r,    \
+                                                                  scal, num,  \
+                                                                  den);       \
+    return static_cast<int>(hipGetLastError());                               \
+  }                                                                           \
+  int bdx_axpy_##SUF(int64_t L1, int64_t ld, int64_t o0, int64_t o1,          \
+                     int64_t o2, T* out, double alpha, const T* x, const T* y, \
+                     hipStream_t st) {                                        \
+    RowSpace s{L1, ld, o0, o1, o2};                                           \
+    axpy_kernel<T><<<grid_for_rows(o0 * o1), kBlock, 0, st>>>(                \
+        s, out, static_cast<T>(alpha), x, y);                                 \
+    return static_cast<int>(hipGetLastError());                               \
+  }                                                                           \
+  int bdx_box_copy_##SUF(int mode, T* vec, int64_t L1, int64_t ld,            \
+                         const int64_t* boxes, int nboxes, int64_t total,     \
+                         T* buf, hipStream_t st) {                            \
+    if (total <= 0) return 0;                                                 \
+    int64_t g64 = (total + kBlock - 1) / kBlock;                              \
+    const int g = static_cast<int>(g64 < 4096 ? g64 : 4096);                  \
+    if (mode == 0)                                                            \
+      box_copy_kernel<T, 0><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
+                                                  total, buf);                \
+    else if (mode == 1)                                                       \
+      box_copy_kernel<T, 1><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
+                                                  total, buf);                \
+    else                                                                      \
+      box_copy_kernel<T, 2><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
+                                                  total, buf);                \
+    return static_cast<int>(hipGetLastError());                               \
+  }
+
+BDX_BLAS_API(double, f64)
+BDX_BLAS_API(float, f32)
+
+}  // extern "C"

@@ -1,0 +1,562 @@
+// Host (CPU) runtime of benchmark_dolfinx_amd.
+//
+// Native replacements for the DOLFINx/Basix machinery the reference leans on
+//  plus its CPU operator:
+//   * stiffness action, sum-factorised, any P in 1..7 and qmode 0/1
+//     (the reference CPU kernel supports only qmode 0: src/laplacian_cpu.hpp:73,
+//     quirk Q4; here both work);
+//   * mass action (RHS b = M f; replaces fem::assemble_vector + the FFCx
+//     kernel, src/laplacian_solver.cpp:100-105);
+//   * interpolation of f at the physical dof nodes (src/main.cpp:81-92);
+//   * CSR assembly of the local stiffness matrix with Dirichlet rows/cols
+//     replaced by the identity (replaces create_sparsity_pattern +
+//     assemble_matrix + set_diagonal, src/laplacian_solver.cpp:161-184);
+//   * CSR SpMV (CPUMatrixOperator, src/laplacian_solver.cpp:247-262).
+// Geometry factors are computed on the fly per cell with 64-bit offsets
+// everywhere (reference quirk Q6: int offset in src/geometry_cpu.hpp:91).
+//
+// Parallelism: OpenMP over the cells of one of 8 parity colours at a time, so
+// no two concurrently processed cells share a dof: the scatter is race-free
+// and deterministic.
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "../include/bdx_lattice.h"
+
+namespace {
+
+template <typename T>
+struct Tables {
+  const T* phi0;   // nq x nd
+  const T* dphi1;  // nq x nq
+  const T* wts;    // nq
+  const T* qpts;   // nq
+  const T* nodes;  // nd
+  bool identity;
+};
+
+// Geometry factor G = w * adj(J) adj(J)^T / det(J) at one point of a
+// trilinear cell with vertices X[8][3] (v = 4a+2b+c), reference point (s,t,u).
+template <typename T>
+inline T geometry_point(const T X[8][3], T s, T t, T u, T w, T G[6]) {
+  T J[3][3];
+  for (int i = 0; i < 3; ++i) {
+    T d0 = 0, d1 = 0, d2 = 0;
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b)
+        for (int c = 0; c < 2; ++c) {
+          const T x = X[4 * a + 2 * b + c][i];
+          const T fx = a ? s : 1 - s, fy = b ? t : 1 - t, fz = c ? u : 1 - u;
+          const T sx = a ? 1 : -1, sy = b ? 1 : -1, sz = c ? 1 : -1;
+          d0 += x * sx * fy * fz;
+          d1 += x * fx * sy * fz;
+          d2 += x * fx * fy * sz;
+        }
+    J[i][0] = d0;
+    J[i][1] = d1;
+    J[i][2] = d2;
+  }
+  // K = adj(J) = det(J) J^{-1}
+  const T K[3][3] = {{J[1][1] * J[2][2] - J[1][2] * J[2][1],
+                      J[0][2] * J[2][1] - J[0][1] * J[2][2],
+                      J[0][1] * J[1][2] - J[0][2] * J[1][1]},
+                     {J[1][2] * J[2][0] - J[1][0] * J[2][2],
+                      J[0][0] * J[2][2] - J[0][2] * J[2][0],
+                      J[0][2] * J[1][0] - J[0][0] * J[1][2]},
+                     {J[1][0] * J[2][1] - J[1][1] * J[2][0],
+                      J[0][1] * J[2][0] - J[0][0] * J[2][1],
+                      J[0][0] * J[1][1] - J[0][1] * J[1][0]}};
+  const T det = J[0][0] * K[0][0] + J[0][1] * K[1][0] + J[0][2] * K[2][0];
+  const T sc = w / det;
+  G[0] = (K[0][0] * K[0][0] + K[0][1] * K[0][1] + K[0][2] * K[0][2]) * sc;
+  G[1] = (K[1][0] * K[0][0] + K[1][1] * K[0][1] + K[1][2] * K[0][2]) * sc;
+  G[2] = (K[2][0] * K[0][0] + K[2][1] * K[0][1] + K[2][2] * K[0][2]) * sc;
+  G[3] = (K[1][0] * K[1][0] + K[1][1] * K[1][1] + K[1][2] * K[1][2]) * sc;
+  G[4] = (K[2][0] * K[1][0] + K[2][1] * K[1][1] + K[2][2] * K[1][2]) * sc;
+  G[5] = (K[2][0] * K[2][0] + K[2][1] * K[2][1] + K[2][2] * K[2][2]) * sc;
+  return det;
+}
+
+template <typename T>
+inline void cell_vertices(const BdxLattice& lat, const T* xv, int64_t cx,
+                          int64_t cy, int64_t cz, T X[8][3]) {
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int c = 0; c < 2; ++c) {
+        const int64_t v = lat.vidx(cx + a, cy + b, cz + c);
+        for (int d = 0; d < 3; ++d) X[4 * a + 2 * b + c][d] = xv[3 * v + d];
+      }
+}
+
+// out = A applied along axis `ax` of `in` (extents e), A is M x K row-major
+// (or K x M used transposed).
+template <typename T>
+inline void contract(const T* A, int M, int K, bool transpose, const T* in,
+                     const int e[3], int ax, T* out) {
+  int eo[3] = {e[0], e[1], e[2]};
+  eo[ax] = M;
+  const int s_in[3] = {e[1] * e[2], e[2], 1};
+  const int s_out[3] = {eo[1] * eo[2], eo[2], 1};
+  for (int i = 0; i < eo[0]; ++i)
+    for (int j = 0; j < eo[1]; ++j)
+      for (int k = 0; k < eo[2]; ++k) {
+        int o[3] = {i, j, k};
+        const int m = o[ax];
+        T acc = 0;
+        for (int q = 0; q < K; ++q) {
+          o[ax] = q;
+          const T a = transpose ? A[q * M + m] : A[m * K + q];
+          acc += a * in[o[0] * s_in[0] + o[1] * s_in[1] + o[2] * s_in[2]];
+        }
+        out[i * s_out[0] + j * s_out[1] + k * s_out[2]] = acc;
+      }
+}
+
+// Interpolate element dofs (nd^3) to quadrature points (nq^3).
+template <typename T, int ND, int NQ>
+inline void interp(const Tables<T>& tb, const T* ue, T* U, T* t1, T* t2) {
+  if (tb.identity) {
+    std::memcpy(U, ue, sizeof(T) * NQ * NQ * NQ);
+    return;
+  }
+  const int e0[3] = {ND, ND, ND};
+  contract(tb.phi0, NQ, ND, false, ue, e0, 0, t1);
+  const int e1[3] = {NQ, ND, ND};
+  contract(tb.phi0, NQ, ND, false, t1, e1, 1, t2);
+  const int e2[3] = {NQ, NQ, ND};
+  contract(tb.phi0, NQ, ND, false, t2, e2, 2, U);
+}
+
+// Transposed interpolation (nq^3 -> nd^3).
+template <typename T, int ND, int NQ>
+inline void interp_t(const Tables<T>& tb, const T* r, T* ye, T* t1, T* t2) {
+  if (tb.identity) {
+    std::memcpy(ye, r, sizeof(T) * ND * ND * ND);
+    return;
+  }
+  const int e0[3] = {NQ, NQ, NQ};
+  contract(tb.phi0, ND, NQ, true, r, e0, 2, t1);
+  const int e1[3] = {NQ, NQ, ND};
+  contract(tb.phi0, ND, NQ, true, t1, e1, 1, t2);
+  const int e2[3] = {NQ, ND, ND};
+  contract(tb.phi0, ND, NQ, true, t2, e2, 0, ye);
+}
+
+// y += kappa * A_cell u for one cell, BC semantics of the reference
+// (src/laplacian_gpu.hpp:153-170, 424-425): BC inputs are zeroed, BC outputs
+// get y = u (only on the owning rank).
+template <typename T, int ND, int NQ>
+void stiffness_cell(const BdxLattice& lat, const Tables<T>& tb, const T* xv,
+                    T kappa, const T* u, T* y, int64_t cx, int64_t cy,
+                    int64_t cz) {
+  constexpr int nd3 = ND * ND * ND, nq3 = NQ * NQ * NQ;
+  const int64_t P = lat.P;
+  T ue[nd3];
+  int64_t dof[nd3];
+  bool bc[nd3];
+  for (int i = 0; i < ND; ++i)
+    for (int j = 0; j < ND; ++j)
+      for (int k = 0; k < ND; ++k) {
+        const int a = (i * ND + j) * ND + k;
+        const int64_t li = cx * P + i, lj = cy * P + j, lk = cz * P + k;
+        dof[a] = lat.idx(li, lj, lk);
+        bc[a] = lat.is_bc(li, lj, lk);
+        ue[a] = bc[a] ? T(0) : u[dof[a]];
+      }
+  T U[nq3], t1[nq3], t2[nq3];
+  interp<T, ND, NQ>(tb, ue, U, t1, t2);
+  T X[8][3];
+  cell_vertices(lat, xv, cx, cy, cz, X);
+  const int eq[3] = {NQ, NQ, NQ};
+  T gx[nq3], gy[nq3], gz[nq3];
+  contract(tb.dphi1, NQ, NQ, false, U, eq, 0, gx);
+  contract(tb.dphi1, NQ, NQ, false, U, eq, 1, gy);
+  contract(tb.dphi1, NQ, NQ, false, U, eq, 2, gz);
+  for (int qx = 0; qx < NQ; ++qx)
+    for (int qy = 0; qy < NQ; ++qy)
+      for (int qz = 0; qz < NQ; ++qz) {
+        const int q = (qx * NQ + qy) * NQ + qz;
+        T G[6];
+        const T w = tb.wts[qx] * tb.wts[qy] * tb.wts[qz];
+        geometry_point<T>(X, tb.qpts[qx], tb.qpts[qy], tb.qpts[qz], w, G);
+        const T a = gx[q], b = gy[q], c = gz[q];
+        gx[q] = kappa * (G[0] * a + G[1] * b + G[2] * c);
+        gy[q] = kappa * (G[1] * a + G[3] * b + G[4] * c);
+        gz[q] = kappa * (G[2] * a + G[4] * b + G[5] * c);
+      }
+  T r[nq3];
+  contract(tb.dphi1, NQ, NQ, true, gx, eq, 0, r);
+  contract(tb.dphi1, NQ, NQ, true, gy, eq, 1, t1);
+  for (int q = 0; q < nq3; ++q) r[q] += t1[q];
+  contract(tb.dphi1, NQ, NQ, true, gz, eq, 2, t1);
+  for (int q = 0; q < nq3; ++q) r[q] += t1[q];
+  T ye[nd3];
+  interp_t<T, ND, NQ>(tb, r, ye, t1, t2);
+  for (int a = 0; a < nd3; ++a) {
+    if (!bc[a]) {
+      y[dof[a]] += ye[a];
+    } else {
+      const int i = a / (ND * ND), j = (a / ND) % ND, k = a % ND;
+      if (lat.is_owned(cx * P + i, cy * P + j, cz * P + k)) y[dof[a]] = u[dof[a]];
+    }
+  }
+}
+
+// b += M_cell f (no BC handling; the caller zeroes BC rows afterwards).
+template <typename T, int ND, int NQ>
+void mass_cell(const BdxLattice& lat, const Tables<T>& tb, const T* xv,
+               const T* f, T* b, int64_t cx, int64_t cy, int64_t cz) {
+  constexpr int nd3 = ND * ND * ND, nq3 = NQ * NQ * NQ;
+  const int64_t P = lat.P;
+  T fe[nd3];
+  int64_t dof[nd3];
+  for (int i = 0; i < ND; ++i)
+    for (int j = 0; j < ND; ++j)
+      for (int k = 0; k < ND; ++k) {
+        const int a = (i * ND + j) * ND + k;
+        dof[a] = lat.idx(cx * P + i, cy * P + j, cz * P + k);
+        fe[a] = f[dof[a]];
+      }
+  T F[nq3], t1[nq3], t2[nq3];
+  interp<T, ND, NQ>(tb, fe, F, t1, t2);
+  T X[8][3];
+  cell_vertices(lat, xv, cx, cy, cz, X);
+  for (int qx = 0; qx < NQ; ++qx)
+    for (int qy = 0; qy < NQ; ++qy)
+      for (int qz = 0; qz < NQ; ++qz) {
+        const int q = (qx * NQ + qy) * NQ + qz;
+        T G[6];
+        const T w = tb.wts[qx] * tb.wts[qy] * tb.wts[qz];
+        const T det =
+            geometry_point<T>(X, tb.qpts[qx], tb.qpts[qy], tb.qpts[qz], T(1), G);
+        F[q] *= w * det;
+      }
+  T be[nd3];
+  interp_t<T, ND, NQ>(tb, F, be, t1, t2);
+  for (int a = 0; a < nd3; ++a) b[dof[a]] += be[a];
+}
+
+// Loop over a box of cells in 8 colour phases (parity of cx, cy, cz): cells
+// of one colour share no dof, so the scatter-add is race-free and the
+// summation order is deterministic.
+template <typename F>
+void for_cells(const int64_t lo[3], const int64_t hi[3], F&& fn) {
+  for (int colour = 0; colour < 8; ++colour) {
+    const int64_t ox = (colour >> 2) & 1, oy = (colour >> 1) & 1, oz = colour & 1;
+#pragma omp parallel for schedule(dynamic, 4) collapse(3)
+    for (int64_t cx = lo[0] + ox; cx < hi[0]; cx += 2)
+      for (int64_t cy = lo[1] + oy; cy < hi[1]; cy += 2)
+        for (int64_t cz = lo[2] + oz; cz < hi[2]; cz += 2) fn(cx, cy, cz);
+  }
+}
+
+// Compile-time (P, nq) dispatch: P in 1..7, nq in {P+1, P+2}.
+template <template <int, int> class Fn, typename... Args>
+void dispatch(int P, int nq, Args&&... args) {
+#define BDX_CASE(PP)                                      \
+  case PP:                                                \
+    if (nq == PP + 1)                                     \
+      return Fn<PP + 1, PP + 1>::run(args...);            \
+    if (nq == PP + 2)                                     \
+      return Fn<PP + 1, PP + 2>::run(args...);            \
+    break;
+  switch (P) {
+    BDX_CASE(1)
+    BDX_CASE(2)
+    BDX_CASE(3)
+    BDX_CASE(4)
+    BDX_CASE(5)
+    BDX_CASE(6)
+    BDX_CASE(7)
+  }
+#undef BDX_CASE
+  throw std::runtime_error("unsupported (degree, nq)");
+}
+
+template <typename T>
+struct StiffArgs {
+  BdxLattice lat;
+  Tables<T> tb;
+  const T* xv;
+  T kappa;
+  const T* u;
+  T* y;
+  int64_t lo[3], hi[3];
+};
+
+template <typename T>
+struct Stiff {
+  template <int ND, int NQ>
+  struct K {
+    static void run(const StiffArgs<T>& a) {
+      for_cells(a.lo, a.hi, [&](int64_t cx, int64_t cy, int64_t cz) {
+        stiffness_cell<T, ND, NQ>(a.lat, a.tb, a.xv, a.kappa, a.u, a.y, cx, cy,
+                                  cz);
+      });
+    }
+  };
+};
+
+template <typename T>
+struct MassArgs {
+  BdxLattice lat;
+  Tables<T> tb;
+  const T* xv;
+  const T* f;
+  T* b;
+  int64_t lo[3], hi[3];
+};
+
+template <typename T>
+struct Mass {
+  template <int ND, int NQ>
+  struct K {
+    static void run(const MassArgs<T>& a) {
+      for_cells(a.lo, a.hi, [&](int64_t cx, int64_t cy, int64_t cz) {
+        mass_cell<T, ND, NQ>(a.lat, a.tb, a.xv, a.f, a.b, cx, cy, cz);
+      });
+    }
+  };
+};
+
+template <typename T>
+Tables<T> make_tables(const T* phi0, const T* dphi1, const T* wts,
+                      const T* qpts, const T* nodes, int identity) {
+  return Tables<T>{phi0, dphi1, wts, qpts, nodes, identity != 0};
+}
+
+// ---------------------------------------------------------------- CSR
+// Column range of local lattice index i along an axis with n cells: the
+// union of the dof ranges of the cells containing it.
+inline void col_range(int64_t i, int64_t P, int64_t n, int64_t& lo,
+                      int64_t& hi) {
+  int64_t c_hi = std::min(i / P, n - 1);
+  int64_t c_lo = (i % P == 0 && i > 0) ? i / P - 1 : c_hi;
+  lo = c_lo * P;
+  hi = c_hi * P + P;  // inclusive
+}
+
+template <typename T>
+int64_t csr_build(const int64_t* latd, int nq, const T* B, const T* Dd,
+                  const T* wts, const T* qpts, const T* xv, T kappa,
+                  int64_t* row_ptr, int32_t* cols, T* vals, int count_only) {
+  const BdxLattice lat = BdxLattice::from(latd);
+  const int64_t P = lat.P, nd = P + 1;
+  const int64_t nrows = lat.size();
+  // pattern (row_ptr must be zero-initialised by the caller: padding rows
+  // of the pitched storage stay empty)
+  row_ptr[0] = 0;
+  for (int64_t i = 0; i < lat.L[0]; ++i)
+    for (int64_t j = 0; j < lat.L[1]; ++j)
+      for (int64_t k = 0; k < lat.L[2]; ++k) {
+        int64_t lo[3], hi[3];
+        const int64_t ijk[3] = {i, j, k};
+        int64_t cnt = 1;
+        for (int d = 0; d < 3; ++d) {
+          col_range(ijk[d], P, lat.n[d], lo[d], hi[d]);
+          cnt *= hi[d] - lo[d] + 1;
+        }
+        row_ptr[lat.idx(i, j, k) + 1] = cnt;
+      }
+  for (int64_t r = 0; r < nrows; ++r) row_ptr[r + 1] += row_ptr[r];
+  const int64_t nnz = row_ptr[nrows];
+  if (count_only) return nnz;
+  if (lat.size() > INT32_MAX) throw std::runtime_error("local size > int32");
+#pragma omp parallel for collapse(2)
+  for (int64_t i = 0; i < lat.L[0]; ++i)
+    for (int64_t j = 0; j < lat.L[1]; ++j)
+      for (int64_t k = 0; k < lat.L[2]; ++k) {
+        int64_t lo[3], hi[3];
+        const int64_t ijk[3] = {i, j, k};
+        for (int d = 0; d < 3; ++d) col_range(ijk[d], P, lat.n[d], lo[d], hi[d]);
+        int64_t p = row_ptr[lat.idx(i, j, k)];
+        for (int64_t a = lo[0]; a <= hi[0]; ++a)
+          for (int64_t b = lo[1]; b <= hi[1]; ++b)
+            for (int64_t c = lo[2]; c <= hi[2]; ++c) {
+              cols[p] = static_cast<int32_t>(lat.idx(a, b, c));
+              vals[p] = 0;
+              ++p;
+            }
+      }
+  // reference gradients gref[a][q][3]
+  const int nd3 = static_cast<int>(nd * nd * nd), nq3 = nq * nq * nq;
+  std::vector<T> gref(static_cast<size_t>(nd3) * nq3 * 3);
+  for (int ia = 0; ia < nd; ++ia)
+    for (int ja = 0; ja < nd; ++ja)
+      for (int ka = 0; ka < nd; ++ka)
+        for (int qx = 0; qx < nq; ++qx)
+          for (int qy = 0; qy < nq; ++qy)
+            for (int qz = 0; qz < nq; ++qz) {
+              const int a = (ia * nd + ja) * nd + ka;
+              const int q = (qx * nq + qy) * nq + qz;
+              T* g = &gref[(static_cast<size_t>(a) * nq3 + q) * 3];
+              g[0] = Dd[qx * nd + ia] * B[qy * nd + ja] * B[qz * nd + ka];
+              g[1] = B[qx * nd + ia] * Dd[qy * nd + ja] * B[qz * nd + ka];
+              g[2] = B[qx * nd + ia] * B[qy * nd + ja] * Dd[qz * nd + ka];
+            }
+  const int64_t lo0[3] = {0, 0, 0};
+  const int64_t hi0[3] = {lat.n[0], lat.n[1], lat.n[2]};
+  for_cells(lo0, hi0, [&](int64_t cx, int64_t cy, int64_t cz) {
+    T X[8][3];
+    cell_vertices(lat, xv, cx, cy, cz, X);
+    std::vector<T> Gq(static_cast<size_t>(nq3) * 6);
+    for (int qx = 0; qx < nq; ++qx)
+      for (int qy = 0; qy < nq; ++qy)
+        for (int qz = 0; qz < nq; ++qz) {
+          const int q = (qx * nq + qy) * nq + qz;
+          geometry_point<T>(X, qpts[qx], qpts[qy], qpts[qz],
+                            wts[qx] * wts[qy] * wts[qz], &Gq[6 * q]);
+        }
+    std::vector<T> tmp(static_cast<size_t>(nd3) * nq3 * 3);
+    for (int b = 0; b < nd3; ++b)
+      for (int q = 0; q < nq3; ++q) {
+        const T* g = &gref[(static_cast<size_t>(b) * nq3 + q) * 3];
+        const T* G = &Gq[6 * q];
+        T* t = &tmp[(static_cast<size_t>(b) * nq3 + q) * 3];
+        t[0] = kappa * (G[0] * g[0] + G[1] * g[1] + G[2] * g[2]);
+        t[1] = kappa * (G[1] * g[0] + G[3] * g[1] + G[4] * g[2]);
+        t[2] = kappa * (G[2] * g[0] + G[4] * g[1] + G[5] * g[2]);
+      }
+    for (int a = 0; a < nd3; ++a) {
+      const int ia = a / static_cast<int>(nd * nd),
+                ja = (a / static_cast<int>(nd)) % nd, ka = a % nd;
+      const int64_t ri = cx * P + ia, rj = cy * P + ja, rk = cz * P + ka;
+      if (lat.is_bc(ri, rj, rk)) continue;
+      const int64_t row = lat.idx(ri, rj, rk);
+      int64_t lo[3], hi[3];
+      const int64_t rijk[3] = {ri, rj, rk};
+      for (int d = 0; d < 3; ++d) col_range(rijk[d], P, lat.n[d], lo[d], hi[d]);
+      const int64_t w1 = hi[1] - lo[1] + 1, w2 = hi[2] - lo[2] + 1;
+      for (int b = 0; b < nd3; ++b) {
+        const int ib = b / static_cast<int>(nd * nd),
+                  jb = (b / static_cast<int>(nd)) % nd, kb = b % nd;
+        const int64_t ci = cx * P + ib, cj = cy * P + jb, ck = cz * P + kb;
+        if (lat.is_bc(ci, cj, ck)) continue;
+        T s = 0;
+        const T* ga = &gref[static_cast<size_t>(a) * nq3 * 3];
+        const T* tb = &tmp[static_cast<size_t>(b) * nq3 * 3];
+        for (int q = 0; q < nq3 * 3; ++q) s += ga[q] * tb[q];
+        const int64_t off = ((ci - lo[0]) * w1 + (cj - lo[1])) * w2 + (ck - lo[2]);
+        vals[row_ptr[row] + off] += s;
+      }
+    }
+  });
+  // identity rows for owned BC dofs
+  for (int64_t i = 0; i < lat.L[0]; ++i)
+    for (int64_t j = 0; j < lat.L[1]; ++j)
+      for (int64_t k = 0; k < lat.L[2]; ++k) {
+        if (!lat.is_bc(i, j, k) || !lat.is_owned(i, j, k)) continue;
+        int64_t lo[3], hi[3];
+        const int64_t ijk[3] = {i, j, k};
+        for (int d = 0; d < 3; ++d) col_range(ijk[d], P, lat.n[d], lo[d], hi[d]);
+        const int64_t w1 = hi[1] - lo[1] + 1, w2 = hi[2] - lo[2] + 1;
+        const int64_t off = ((i - lo[0]) * w1 + (j - lo[1])) * w2 + (k - lo[2]);
+        vals[row_ptr[lat.idx(i, j, k)] + off] = 1;
+      }
+  return nnz;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bdx_host_version() { return 1; }
+
+#define BDX_HOST_API(T, SUF)                                                  \
+  void bdx_cpu_stiffness_##SUF(const int64_t* latd, int nq, const T* phi0,    \
+                               const T* dphi1, const T* wts, const T* qpts,   \
+                               const T* nodes, int identity, const T* xv,     \
+                               T kappa, const T* u, T* y, const int64_t* lo,  \
+                               const int64_t* hi) {                           \
+    StiffArgs<T> a;                                                           \
+    a.lat = BdxLattice::from(latd);                                           \
+    a.tb = make_tables<T>(phi0, dphi1, wts, qpts, nodes, identity);           \
+    a.xv = xv;                                                                \
+    a.kappa = kappa;                                                          \
+    a.u = u;                                                                  \
+    a.y = y;                                                                  \
+    for (int d = 0; d < 3; ++d) {                                             \
+      a.lo[d] = lo[d];                                                        \
+      a.hi[d] = hi[d];                                                        \
+    }                                                                         \
+    dispatch<Stiff<T>::template K>(static_cast<int>(a.lat.P), nq, a);         \
+  }                                                                           \
+  void bdx_cpu_mass_##SUF(const int64_t* latd, int nq, const T* phi0,         \
+                          const T* dphi1, const T* wts, const T* qpts,        \
+                          const T* nodes, int identity, const T* xv,          \
+                          const T* f, T* b, const int64_t* lo,                \
+                          const int64_t* hi) {                                \
+    MassArgs<T> a;                                                            \
+    a.lat = BdxLattice::from(latd);                                           \
+    a.tb = make_tables<T>(phi0, dphi1, wts, qpts, nodes, identity);           \
+    a.xv = xv;                                                                \
+    a.f = f;                                                                  \
+    a.b = b;                                                                  \
+    for (int d = 0; d < 3; ++d) {                                             \
+      a.lo[d] = lo[d];                                                        \
+      a.hi[d] = hi[d];                                                        \
+    }                                                                         \
+    dispatch<Mass<T>::template K>(static_cast<int>(a.lat.P), nq, a);          \
+  }                                                                           \
+  int64_t bdx_cpu_csr_##SUF(const int64_t* latd, int nq, const T* B,          \
+                            const T* Dd, const T* wts, const T* qpts,         \
+                            const T* xv, T kappa, int64_t* row_ptr,           \
+                            int32_t* cols, T* vals, int count_only) {         \
+    return csr_build<T>(latd, nq, B, Dd, wts, qpts, xv, kappa, row_ptr, cols, \
+                        vals, count_only);                                    \
+  }                                                                           \
+  void bdx_cpu_spmv_##SUF(int64_t nrows, const int64_t* row_ptr,              \
+                          const int32_t* cols, const T* vals, const T* x,     \
+                          T* y) {                                             \
+    _Pragma("omp parallel for schedule(static)") for (int64_t r = 0;          \
+                                                      r < nrows; ++r) {       \
+      T s = 0;                                                                \
+      for (int64_t p = row_ptr[r]; p < row_ptr[r + 1]; ++p)                   \
+        s += vals[p] * x[cols[p]];                                            \
+      y[r] = s;                                                               \
+    }                                                                         \
+  }                                                                           \
+  /* f = 1000 exp(-((x-1/2)^2 + (y-1/2)^2)/0.02) at the physical dof nodes */ \
+  void bdx_cpu_interp_f_##SUF(const int64_t* latd, const T* nodes,            \
+                              const T* xv, T* f) {                            \
+    const BdxLattice lat = BdxLattice::from(latd);                            \
+    const int64_t P = lat.P;                                                  \
+    _Pragma("omp parallel for collapse(2)") for (int64_t i = 0;               \
+                                                 i < lat.L[0]; ++i) {         \
+      for (int64_t j = 0; j < lat.L[1]; ++j) {                                \
+        for (int64_t k = 0; k < lat.L[2]; ++k) {                              \
+          const int64_t ijk[3] = {i, j, k};                                   \
+          int64_t c[3];                                                       \
+          T s[3];                                                             \
+          for (int d = 0; d < 3; ++d) {                                       \
+            c[d] = std::min<int64_t>(ijk[d] / P, lat.n[d] - 1);               \
+            s[d] = nodes[ijk[d] - c[d] * P];                                  \
+          }                                                                   \
+          T X[8][3];                                                          \
+          cell_vertices(lat, xv, c[0], c[1], c[2], X);                        \
+          T x[3] = {0, 0, 0};                                                 \
+          for (int a = 0; a < 2; ++a)                                         \
+            for (int b = 0; b < 2; ++b)                                       \
+              for (int cc = 0; cc < 2; ++cc) {                                \
+                const T wgt = (a ? s[0] : 1 - s[0]) * (b ? s[1] : 1 - s[1]) * \
+                              (cc ? s[2] : 1 - s[2]);                         \
+                for (int d = 0; d < 3; ++d)                                   \
+                  x[d] += wgt * X[4 * a + 2 * b + cc][d];                     \
+              }                                                               \
+          const T dx = x[0] - T(0.5), dy = x[1] - T(0.5);                     \
+          f[lat.idx(i, j, k)] =                                               \
+              T(1000) * std::exp(-(dx * dx + dy * dy) / T(0.02));             \
+        }                                                                     \
+      }                                                                       \
+    }                                                                         \
+  }
+
+BDX_HOST_API(double, f64)
+BDX_HOST_API(float, f32)
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+"""Benchmark drivers: setup -> timed loop -> norms -> optional CSR comparison.
+
+Reference: `laplace_action_gpu` / `laplace_action_cpu`
+(src/laplacian_solver.cpp:64-391) and `run_benchmark` (src/main.cpp:41-133).
+
+Timing fixes quirk Q9: all ranks synchronise the device and meet at a
+barrier before the clock starts and after it stops, and the reported time is
+the MAX over ranks (the reference reads rank 0's clock with no barrier).
+"""
+
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from .models.poisson import (CSROperator, MatFreeLaplacianCPU, MatFreeLaplacianGPU,
+                             PoissonProblem)
+from .solvers.cg import DeviceCG, cg_solve
+from .utils.timing import add_time, timed
+
+
+@dataclass
+class BenchmarkResults:
+    mat_free_time: float = 0.0
+    unorm: float = 0.0
+    ynorm: float = 0.0
+    znorm: float = 0.0
+    enorm: float = 0.0
+    extra: dict = field(default_factory=dict)
+
+
+def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "auto"):
+    if pb.platform == "cpu":
+        return MatFreeLaplacianCPU(pb)
+    if kernel == "auto":
+        kernel = "fused"
+    if kernel == "fused":
+        from .models.fused import FusedLaplacianGPU, fused_supported
+        if fused_supported(pb):
+            return FusedLaplacianGPU(pb, geometry="otf" if geometry == "auto" else geometry)
+        kernel = "v1"
+    if kernel == "v1":
+        return MatFreeLaplacianGPU(pb, geometry="stored" if geometry == "auto" else geometry)
+    raise ValueError(f"unknown kernel {kernel}")
+
+
+def _sync(pb: PoissonProblem) -> None:
+    if pb.platform == "gpu":
+        torch.cuda.synchronize()
+    pb.comm.barrier()
+    if pb.platform == "gpu":
+        torch.cuda.synchronize()
+
+
+def _run_loop(op, pb, x, u, nreps, use_cg, dev_cg):
+    if use_cg:
+        if pb.platform == "gpu":
+            dev_cg.solve(op, x, u, nreps)
+        else:
+            cg_solve(op, pb, x, u, nreps, 0.0)
+    else:
+        for _ in range(nreps):
+            op.apply(u, x)
+
+
+def laplace_action(pb: PoissonProblem, nreps: int, use_cg: bool, mat_comp: bool,
+                   kernel: str = "auto", geometry: str = "auto", warmup: int = 0,
+                   printer=print) -> BenchmarkResults:
+    rank0 = pb.comm.rank == 0
+    res = BenchmarkResults()
+    u = pb.assemble_rhs()
+    y = pb.new_vector()
+    with timed("% Create matfree operator"):
+        op = make_operator(pb, kernel, geometry)
+        if pb.platform == "gpu":
+            torch.cuda.synchronize()
+    dev_cg = DeviceCG(pb) if (use_cg and pb.platform == "gpu") else None
+    res.extra["kernel"] = getattr(op, "name", type(op).__name__)
+    res.extra["geometry"] = getattr(op, "geometry", "otf")
+    if warmup > 0:
+        with timed("~warmup"):
+            _run_loop(op, pb, y, u, warmup, use_cg, dev_cg)
+            y.zero_()
+    _sync(pb)
+    t0 = time.perf_counter()
+    _run_loop(op, pb, y, u, nreps, use_cg, dev_cg)
+    _sync(pb)
+    dt = time.perf_counter() - t0
+    dt = pb.comm.allreduce_scalar(dt, "max")
+    add_time("% Matrix-free " + ("CG" if use_cg else "action"), dt, 1)
+    res.mat_free_time = dt
+    res.unorm = pb.norm(u)
+    res.ynorm = pb.norm(y)
+    if rank0:
+        comp = "CG" if use_cg else "Action"
+        printer(f"Computation time ({comp}): {dt:.6g}s")
+        printer(f"Computation rate (Gdofs/s): {pb.ndofs_global * nreps / (1e9 * dt):.6g}")
+        printer(f"Norm of u = {res.unorm:.6g}")
+        printer(f"Norm of y = {res.ynorm:.6g}")
+
+    if mat_comp:
+        A = CSROperator(pb)
+        z = pb.new_vector()
+        _sync(pb)
+        with timed("% CSR Matvec", sync=lambda: _sync(pb)):
+            if use_cg:
+                cg_solve(A, pb, z, u, nreps, 0.0)
+            else:
+                for _ in range(nreps):
+                    A.apply(u, z)
+        res.znorm = pb.norm(z)
+        e = z - y
+        res.enorm = pb.norm(e)
+        if rank0:
+            printer(f"Norm of u = {res.unorm:.6g}")
+            printer(f"Norm of z = {res.znorm:.6g}")
+            printer(f"Norm of error = {res.enorm:.6g}")
+            rel = res.enorm / res.znorm if res.znorm != 0 else float("nan")
+            printer(f"Relative norm of error = {rel:.6g}")
+    return res

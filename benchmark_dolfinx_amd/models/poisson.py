@@ -1,0 +1,268 @@
+"""The benchmark problem: -div(kappa grad u) = f on the unit cube, Q_P hexes.
+
+Reference: `run_benchmark<T>` (src/main.cpp:41-133) and the operator classes
+MatFreeLaplacianGPU/CPU (src/laplacian.hpp:87-771) and MatrixOperator
+(src/csr.hpp:113-234).
+
+* `PoissonProblem` builds the rank-local lattice, the 1D tables, the mesh
+  vertices (optionally perturbed), interpolates f and assembles the RHS
+  b = M f with Dirichlet rows zeroed (src/laplacian_solver.cpp:100-105).
+* `MatFreeLaplacianCPU` / `MatFreeLaplacianGPU` apply y = A u with the
+  reference's BC semantics (A = kappa K with Dirichlet rows/columns replaced
+  by the identity).  One forward halo exchange of u overlapped with the
+  interior cells, one reverse exchange of the ghost-plane partial sums.
+* `CSROperator` is the assembled-matrix comparison operator (--mat_comp).
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..fem.mesh import LocalLattice, make_local_lattice, vertex_coordinates
+from ..fem.quadrature import OperatorTables
+from ..ops import native
+from ..ops.native import ptr
+from ..parallel.comm import Comm
+from ..parallel.halo import HaloExchange
+from ..utils.timing import timed
+
+KAPPA = 2.0  # src/main.cpp:71
+
+
+def _np_dtype(dtype):
+    return np.float64 if dtype == torch.float64 else np.float32
+
+
+class PoissonProblem:
+    def __init__(self, comm: Comm, ncells, degree: int, qmode: int = 1,
+                 use_gauss: bool = False, dtype=torch.float64, platform: str = "gpu",
+                 perturb: float = 0.0):
+        if use_gauss and qmode == 0:
+            # same validation as the reference (src/laplacian.hpp:197-198, Q5)
+            raise RuntimeError("Expecting identity matrix for qmode=0")
+        self.comm = comm
+        self.platform = platform
+        self.device = torch.device("cuda", torch.cuda.current_device()) \
+            if platform == "gpu" else torch.device("cpu")
+        self.dtype = dtype
+        self.kappa = KAPPA
+        self.degree = degree
+        self.qmode = qmode
+        self.use_gauss = use_gauss
+        self.tables = OperatorTables(degree, qmode, use_gauss)
+        self.lat: LocalLattice = make_local_lattice(comm.rank, comm.size, tuple(ncells), degree)
+        npdt = _np_dtype(dtype)
+        with timed("~setup mesh"):
+            xv = vertex_coordinates(self.lat, perturb).astype(npdt)
+            self.xv_host = np.ascontiguousarray(xv)
+            self.xv = torch.from_numpy(self.xv_host).to(self.device)
+        self.host_tables = {k: np.ascontiguousarray(v, dtype=npdt) for k, v in dict(
+            phi0=self.tables.phi0, dphi1=self.tables.dphi1, wts=self.tables.qwts,
+            qpts=self.tables.qpts, nodes=self.tables.nodes, B=self.tables.B,
+            Dd=self.tables.Dd).items()}
+        self.kernels = None
+        if platform == "gpu":
+            from ..ops.kernels import HipKernels
+            self.kernels = HipKernels(self.lat, self.tables, dtype)
+        self.halo = HaloExchange(self.lat, comm, dtype, self.device, self.kernels)
+        # kept alive for ctypes calls (never pass temporaries to ptr())
+        self.latd = self.lat.as_int64()
+
+    # --------------------------------------------------------------- vectors
+    @property
+    def suf(self) -> str:
+        return "f64" if self.dtype == torch.float64 else "f32"
+
+    def new_vector(self) -> torch.Tensor:
+        return torch.zeros(self.lat.shape, dtype=self.dtype, device=self.device)
+
+    def owned(self, v: torch.Tensor) -> torch.Tensor:
+        o = self.lat.owned_hi
+        return v[: o[0], : o[1], : o[2]]
+
+    def inner(self, a: torch.Tensor, b: torch.Tensor) -> float:
+        s = torch.sum(self.owned(a).double() * self.owned(b).double())
+        if self.comm.size > 1:
+            self.comm.allreduce_(s.view(1) if s.dim() == 0 else s)
+        return float(s.item())
+
+    def norm(self, v: torch.Tensor) -> float:
+        return math.sqrt(max(self.inner(v, v), 0.0))
+
+    def bc_mask(self) -> torch.Tensor:
+        m = np.zeros(self.lat.shape, dtype=bool)
+        m[:, :, : self.lat.L[2]] = self.lat.bc_mask()
+        return torch.from_numpy(m).to(self.device)
+
+    def to_global_array(self, v: torch.Tensor) -> np.ndarray:
+        """Gather the owned values into a global lexicographic numpy array (tests)."""
+        o = self.lat.owned_hi
+        loc = self.owned(v).detach().cpu().numpy().astype(np.float64)
+        gidx = self.lat.global_indices()[: o[0], : o[1], : o[2]]
+        parts = self.comm.gather_objects((gidx.ravel(), loc.ravel()))
+        out = np.zeros(self.lat.ndofs_global)
+        for gi, val in parts:
+            out[gi] = val
+        return out
+
+    # -------------------------------------------------------------- RHS
+    def interpolate_f(self) -> torch.Tensor:
+        """f at the physical dof nodes (src/main.cpp:81-92), all local points."""
+        f = np.zeros(self.lat.shape, dtype=_np_dtype(self.dtype))
+        lib = native.host()
+        getattr(lib, f"bdx_cpu_interp_f_{self.suf}")(
+            ptr(self.latd), ptr(self.host_tables["nodes"]), ptr(self.xv_host), ptr(f))
+        return torch.from_numpy(f).to(self.device)
+
+    def assemble_rhs(self) -> torch.Tensor:
+        """b = M f, reverse-scattered, Dirichlet rows zeroed."""
+        with timed("~setup assemble RHS"):
+            f = self.interpolate_f()
+            b = self.new_vector()
+            lo = np.zeros(3, dtype=np.int64)
+            hi = np.array(self.lat.n, dtype=np.int64)
+            if self.platform == "gpu":
+                self.kernels.v1_apply(2, None, self.xv, 0.0, f, b, lo, hi)
+            else:
+                t = self.host_tables
+                getattr(native.host(), f"bdx_cpu_mass_{self.suf}")(
+                    ptr(self.latd), self.tables.nq, ptr(t["phi0"]), ptr(t["dphi1"]),
+                    ptr(t["wts"]), ptr(t["qpts"]), ptr(t["nodes"]), int(self.tables.is_identity),
+                    ptr(self.xv_host), ptr(f.numpy()), ptr(b.numpy()), ptr(lo), ptr(hi))
+            self.halo.reverse(b)
+            b.masked_fill_(self.bc_mask(), 0.0)
+            self.halo.forward(b)
+        return b
+
+    @property
+    def ndofs_global(self) -> int:
+        return self.lat.ndofs_global
+
+    @property
+    def ncells_global(self) -> int:
+        return self.lat.ncells_global_total
+
+
+class MatFreeLaplacianCPU:
+    """CPU operator (C++/OpenMP, both qmodes; src/laplacian.hpp:450-771)."""
+
+    def __init__(self, problem: PoissonProblem):
+        self.pb = problem
+        self.lib = native.host()
+        self._fn = getattr(self.lib, f"bdx_cpu_stiffness_{problem.suf}")
+        self.latd = problem.lat.as_int64()
+
+    def _cells(self, u, y, lo, hi):
+        t = self.pb.host_tables
+        lo = np.asarray(lo, dtype=np.int64)
+        hi = np.asarray(hi, dtype=np.int64)
+        self._fn(ptr(self.latd), self.pb.tables.nq, ptr(t["phi0"]), ptr(t["dphi1"]),
+                 ptr(t["wts"]), ptr(t["qpts"]), ptr(t["nodes"]),
+                 int(self.pb.tables.is_identity), ptr(self.pb.xv_host), self.pb.kappa,
+                 ptr(u.numpy()), ptr(y.numpy()), ptr(lo), ptr(hi))
+
+    def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
+        lat = self.pb.lat
+        y.zero_()
+        work = self.pb.halo.forward_begin(u)
+        lo, hi = lat.interior_cell_box()
+        self._cells(u, y, lo, hi)
+        self.pb.halo.forward_end(u, work)
+        for lo, hi in lat.boundary_cell_boxes():
+            self._cells(u, y, lo, hi)
+        self.pb.halo.reverse(y)
+
+
+class MatFreeLaplacianGPU:
+    """Matrix-free operator on the GPU.
+
+    geometry="stored": G precomputed once (6 nq^3 values per cell, the
+    reference's memory layout and maths); "otf": G recomputed per
+    quadrature point from the 8 vertices of the cell (no G array).
+    """
+
+    def __init__(self, problem: PoissonProblem, geometry: str = "stored"):
+        self.pb = problem
+        self.k = problem.kernels
+        self.geometry = geometry
+        self.G = None
+        if geometry == "stored":
+            lat = problem.lat
+            nq3 = problem.tables.nq ** 3
+            with timed("~setup geometry"):
+                self.G = torch.empty(lat.ncells_local * 6 * nq3, dtype=problem.dtype,
+                                     device=problem.device)
+                self.k.geometry(problem.xv, self.G)
+        elif geometry != "otf":
+            raise ValueError(f"unknown geometry mode {geometry}")
+        self.mode = 0 if geometry == "stored" else 1
+
+    def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
+        pb, lat = self.pb, self.pb.lat
+        y.zero_()
+        work = pb.halo.forward_begin(u)
+        lo, hi = lat.interior_cell_box()
+        self.k.v1_apply(self.mode, self.G, pb.xv, pb.kappa, u, y, lo, hi)
+        pb.halo.forward_end(u, work)
+        for lo, hi in lat.boundary_cell_boxes():
+            self.k.v1_apply(self.mode, self.G, pb.xv, pb.kappa, u, y, lo, hi)
+        pb.halo.reverse(y)
+
+
+class CSROperator:
+    """Assembled local stiffness matrix (rows = local lattice incl. ghost rows).
+
+    Assembly on the CPU (C++), SpMV on the device of the problem; the ghost
+    rows' partial sums go through the same reverse halo exchange as the
+    matrix-free operator (the reference assembles owned rows via
+    MatrixCSR::scatter_rev, src/laplacian_solver.cpp:183).
+    """
+
+    def __init__(self, problem: PoissonProblem):
+        self.pb = problem
+        lat = problem.lat
+        if lat.nstore >= 2 ** 31:
+            raise RuntimeError("Too many matrix rows for int32 columns")
+        lib = native.host()
+        fn = getattr(lib, f"bdx_cpu_csr_{problem.suf}")
+        t = problem.host_tables
+        npdt = _np_dtype(problem.dtype)
+        row_ptr = np.zeros(lat.nstore + 1, dtype=np.int64)
+        self.latd = problem.latd
+        args = (ptr(self.latd), problem.tables.nq, ptr(t["B"]), ptr(t["Dd"]),
+                ptr(t["wts"]), ptr(t["qpts"]), ptr(problem.xv_host), problem.kappa)
+        with timed("% Create CPU MatrixCSR"):
+            nnz = fn(*args, ptr(row_ptr), 0, 0, 1)
+            if nnz >= 2 ** 31:
+                raise RuntimeError("Too many matrix entries, need 64-bit row_ptr.")
+            cols = np.zeros(nnz, dtype=np.int32)
+            vals = np.zeros(nnz, dtype=npdt)
+            row_ptr[:] = 0
+        with timed("% Assemble CPU MatrixCSR"):
+            fn(*args, ptr(row_ptr), ptr(cols), ptr(vals), 0)
+        self.nnz = int(nnz)
+        self.nrows = lat.nstore
+        with timed("% Copy to GPU MatrixCSR" if problem.platform == "gpu"
+                   else "% Copy CSR"):
+            self.row_ptr = torch.from_numpy(row_ptr).to(problem.device)
+            self.cols = torch.from_numpy(cols).to(problem.device)
+            self.vals = torch.from_numpy(vals).to(problem.device)
+        self._host = (row_ptr, cols, vals)
+
+    def frobenius_norm(self) -> float:
+        s = float(torch.sum(self.vals.double() ** 2).item())
+        return math.sqrt(self.pb.comm.allreduce_scalar(s))
+
+    def apply(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        pb = self.pb
+        pb.halo.forward(x)
+        if pb.platform == "gpu":
+            pb.kernels.spmv(self.nrows, self.row_ptr, self.cols, self.vals, x, y)
+        else:
+            getattr(native.host(), f"bdx_cpu_spmv_{pb.suf}")(
+                self.nrows, ptr(self.row_ptr.numpy()), ptr(self.cols.numpy()),
+                ptr(self.vals.numpy()), ptr(x.numpy()), ptr(y.numpy()))
+        pb.halo.reverse(y)

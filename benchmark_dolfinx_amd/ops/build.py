@@ -1,0 +1,137 @@
+"""In-tree build of the native libraries.
+
+* ``libbdx_host.so``: C++17 host runtime (g++, -O3, OpenMP): CPU operator,
+  CSR assembly, SpMV, interpolation.
+* ``libbdx_hip.so``: HIP kernels for gfx950 only (hipcc
+  --offload-arch=gfx950, -munsafe-fp-atomics like the reference's
+  src/CMakeLists.txt:53-61).  Translation units are compiled in parallel and
+  linked into one shared object.
+
+Both land next to this file so they travel with the repo snapshot to the
+GPU box (they are git-ignored).  Nothing is written under ~/.cache.
+
+Usage: ``python -m benchmark_dolfinx_amd.ops.build [--host] [--hip] [-j N]``
+"""
+
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+PKG = HERE.parent
+CSRC = PKG / "csrc"
+HOST_SO = HERE / "libbdx_host.so"
+HIP_SO = HERE / "libbdx_hip.so"
+OBJ_DIR = PKG / "csrc" / "build"
+
+HIP_ARCH = os.environ.get("BDX_HIP_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _sources(sub: str, ext: str) -> list[Path]:
+    return sorted((CSRC / sub).glob(f"*{ext}"))
+
+
+def _headers() -> list[Path]:
+    return sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "hip").glob("*.h"))
+
+
+def _digest(paths: list[Path], extra: str = "") -> str:
+    h = hashlib.sha1(extra.encode())
+    for p in paths:
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _up_to_date(target: Path, digest: str) -> bool:
+    stamp = target.with_suffix(target.suffix + ".sha1")
+    return target.exists() and stamp.exists() and stamp.read_text().strip() == digest
+
+
+def _stamp(target: Path, digest: str) -> None:
+    target.with_suffix(target.suffix + ".sha1").write_text(digest + "\n")
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build failed: {cmd[0]} ... {cmd[-1]}")
+
+
+def build_host(force: bool = False) -> Path:
+    srcs = _sources("host", ".cpp")
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-march=x86-64-v2",
+             "-Wall", "-Wno-unknown-pragmas"]
+    digest = _digest(srcs + _headers(), " ".join(flags))
+    if not force and _up_to_date(HOST_SO, digest):
+        return HOST_SO
+    cxx = shutil.which("g++") or "c++"
+    tmp = HOST_SO.with_suffix(".so.tmp")
+    _run([cxx, *flags, "-I", str(CSRC / "include"), *map(str, srcs), "-o", str(tmp)])
+    os.replace(tmp, HOST_SO)
+    _stamp(HOST_SO, digest)
+    return HOST_SO
+
+
+def hip_flags() -> list[str]:
+    return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={HIP_ARCH}",
+            "-munsafe-fp-atomics", "-ffp-contract=fast", "-Wno-unused-result",
+            "-I", str(CSRC / "include"), "-I", str(CSRC / "hip")]
+
+
+def build_hip(force: bool = False, jobs: int | None = None) -> Path:
+    srcs = _sources("hip", ".hip")
+    flags = hip_flags()
+    digest = _digest(srcs + _headers(), " ".join(flags))
+    if not force and _up_to_date(HIP_SO, digest):
+        return HIP_SO
+    if not Path(HIPCC).exists():
+        raise RuntimeError(f"hipcc not found at {HIPCC}")
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(srcs)))
+
+    def compile_one(src: Path) -> Path:
+        obj = OBJ_DIR / (src.stem + ".o")
+        odig = _digest([src] + _headers(), " ".join(flags))
+        if not force and _up_to_date(obj, odig):
+            return obj
+        _run([HIPCC, *flags, "-c", str(src), "-o", str(obj)])
+        _stamp(obj, odig)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = HIP_SO.with_suffix(".so.tmp")
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={HIP_ARCH}", *map(str, objs),
+          "-o", str(tmp)])
+    os.replace(tmp, HIP_SO)
+    _stamp(HIP_SO, digest)
+    return HIP_SO
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", action="store_true")
+    ap.add_argument("--hip", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    both = not (a.host or a.hip)
+    if a.host or both:
+        print("built", build_host(a.force))
+    if a.hip or both:
+        print("built", build_hip(a.force, a.jobs))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,39 @@
+"""ctypes signatures of libbdx_hip.so (see csrc/hip/*.hip)."""
+
+from __future__ import annotations
+
+import ctypes
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int
+i64 = ctypes.c_int64
+f64 = ctypes.c_double
+f32 = ctypes.c_float
+
+
+def _d(lib, name, argtypes, restype=i32):
+    fn = getattr(lib, name)
+    fn.argtypes = argtypes
+    fn.restype = restype
+
+
+def declare(lib) -> None:
+    _d(lib, "bdx_hip_partials_size", [])
+    _d(lib, "bdx_device_info", [i32, ctypes.c_char_p, i32])
+    for suf in ("f64", "f32"):
+        ft = f64 if suf == "f64" else f32
+        _d(lib, f"bdx_dot_{suf}", [i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, vp])
+        _d(lib, f"bdx_cg_update_{suf}",
+           [i64, i64, i64, i64, i64, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp])
+        _d(lib, f"bdx_p_update_{suf}", [i64, i64, i64, i64, i64, vp, vp, vp, i32, i32, vp])
+        _d(lib, f"bdx_axpy_{suf}", [i64, i64, i64, i64, i64, vp, f64, vp, vp, vp])
+        _d(lib, f"bdx_box_copy_{suf}", [i32, vp, i64, i64, vp, i32, i64, vp, vp])
+        _d(lib, f"bdx_v1_apply_{suf}",
+           [i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp])
+        _d(lib, f"bdx_geometry_{suf}", [vp, i32, vp, vp, vp, vp, vp, vp, vp])
+        _d(lib, f"bdx_spmv_{suf}", [i64, vp, vp, vp, vp, vp, vp])
+        if hasattr(lib, f"bdx_fused_apply_{suf}"):
+            _d(lib, f"bdx_fused_apply_{suf}",
+               [i32, vp, i32, vp, vp, vp, vp, i32, vp, f64, vp, vp, vp, vp, vp,
+                vp, i32, i32, vp, vp, vp])
+    del ft

@@ -1,0 +1,120 @@
+"""Python front-end of the HIP kernels: torch tensors in, kernels on the
+current HIP stream, errors raised loudly (no silent fallback)."""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import native
+from .native import ptr
+
+
+def _suf(dtype) -> str:
+    if dtype == torch.float64:
+        return "f64"
+    if dtype == torch.float32:
+        return "f32"
+    raise TypeError(f"unsupported dtype {dtype}")
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise HipError(f"{what} failed with hipError {rc}")
+
+
+class TableSet:
+    """float64 copies of the 1D tables kept alive for ctypes calls."""
+
+    def __init__(self, tables):
+        self.nq = tables.nq
+        self.nd = tables.nd
+        self.identity = int(tables.is_identity)
+        self.phi0 = np.ascontiguousarray(tables.phi0, dtype=np.float64)
+        self.dphi1 = np.ascontiguousarray(tables.dphi1, dtype=np.float64)
+        self.wts = np.ascontiguousarray(tables.qwts, dtype=np.float64)
+        self.qpts = np.ascontiguousarray(tables.qpts, dtype=np.float64)
+
+
+class HipKernels:
+    """Bound kernel launchers for one problem (lattice + tables + dtype)."""
+
+    def __init__(self, lat, tables, dtype):
+        self.lib = native.hip()
+        self.lat = lat
+        self.latd = lat.as_int64()
+        self.t = TableSet(tables)
+        self.dtype = dtype
+        self.suf = _suf(dtype)
+        self.npart = self.lib.bdx_hip_partials_size()
+        self.o = lat.owned_hi
+
+    def _f(self, name):
+        return getattr(self.lib, f"{name}_{self.suf}")
+
+    # --------------------------------------------------------------- operator
+    def v1_apply(self, mode: int, G, xv, kappa: float, u, y, lo, hi):
+        lo = np.asarray(lo, dtype=np.int64)
+        hi = np.asarray(hi, dtype=np.int64)
+        t = self.t
+        _check(self._f("bdx_v1_apply")(mode, ptr(self.latd), t.nq, ptr(t.phi0),
+                                       ptr(t.dphi1), ptr(t.wts), ptr(t.qpts), t.identity,
+                                       ptr(G), ptr(xv), kappa, ptr(u), ptr(y), ptr(lo),
+                                       ptr(hi), _stream()), "v1_apply")
+
+    def geometry(self, xv, G):
+        t = self.t
+        _check(self._f("bdx_geometry")(ptr(self.latd), t.nq, ptr(t.phi0), ptr(t.dphi1),
+                                       ptr(t.wts), ptr(t.qpts), ptr(xv), ptr(G), _stream()),
+               "geometry")
+
+    # ------------------------------------------------------------------ BLAS
+    def dot(self, a, b, partials, out, slot: int):
+        L = self.lat
+        _check(self._f("bdx_dot")(L.L[1], L.ld, self.o[0], self.o[1], self.o[2], ptr(a),
+                                  ptr(b), ptr(partials), ptr(out), slot, _stream()), "dot")
+
+    def cg_update(self, x, r, p, y, scal, rn_slot, pap_slot, out_slot, partials):
+        L = self.lat
+        _check(self._f("bdx_cg_update")(L.L[1], L.ld, self.o[0], self.o[1], self.o[2],
+                                        ptr(x), ptr(r), ptr(p), ptr(y), ptr(scal), rn_slot,
+                                        pap_slot, out_slot, ptr(partials), _stream()),
+               "cg_update")
+
+    def p_update(self, p, r, scal, num, den):
+        L = self.lat
+        _check(self._f("bdx_p_update")(L.L[1], L.ld, self.o[0], self.o[1], self.o[2],
+                                       ptr(p), ptr(r), ptr(scal), num, den, _stream()),
+               "p_update")
+
+    def axpy(self, out, alpha: float, x, y):
+        L = self.lat
+        _check(self._f("bdx_axpy")(L.L[1], L.ld, self.o[0], self.o[1], self.o[2], ptr(out),
+                                   float(alpha), ptr(x), ptr(y), _stream()), "axpy")
+
+    def box_copy(self, mode: int, vec, lat, side, buf):
+        _check(self._f("bdx_box_copy")(mode, ptr(vec), lat.L[1], lat.ld, ptr(side.table),
+                                       len(side.boxes), side.total, ptr(buf), _stream()),
+               "box_copy")
+
+    def spmv(self, nrows, row_ptr, cols, vals, x, y):
+        _check(self._f("bdx_spmv")(nrows, ptr(row_ptr), ptr(cols), ptr(vals), ptr(x),
+                                   ptr(y), _stream()), "spmv")
+
+
+def device_info(dev: int = 0) -> str:
+    import ctypes
+    lib = native.hip()
+    buf = ctypes.create_string_buffer(1024)
+    rc = lib.bdx_device_info(dev, buf, 1024)
+    if rc != 0:
+        return f"(device info unavailable: hipError {rc})\n"
+    return buf.value.decode()

@@ -1,0 +1,90 @@
+"""Process-group plumbing: one process per GPU over torch.distributed.
+
+The reference is SPMD over GPU-aware MPI with an external `select_gpu`
+wrapper for device binding (README.md:94-104, quirk Q13).  Here:
+
+* ranks come from the torchrun environment (RANK / WORLD_SIZE /
+  LOCAL_RANK / MASTER_ADDR / MASTER_PORT), the device is bound from
+  LOCAL_RANK before the process group is created;
+* backend ``nccl`` (= RCCL on ROCm, over xGMI intra-node) for the GPU
+  platform, ``gloo`` for the CPU platform (multi-process CPU tests);
+* every collective works on tensors resident where the data lives: CG dot
+  products are all-reduced as float64 *device* scalars (no host round trip,
+  unlike the host-scalar MPI_Allreduce of src/cg.hpp:76); halo traffic is
+  one all-to-all(v) per exchange (parallel/halo.py).
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    """Thin wrapper; a size-1 Comm makes every collective a no-op."""
+
+    def __init__(self):
+        self.enabled = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank() if self.enabled else 0
+        self.size = dist.get_world_size() if self.enabled else 1
+        self.backend = dist.get_backend() if self.enabled else "none"
+
+    # ----------------------------------------------------------- collectives
+    def allreduce_(self, t: torch.Tensor, op: str = "sum", async_op: bool = False):
+        if self.size == 1:
+            return None
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+               "min": dist.ReduceOp.MIN}[op]
+        return dist.all_reduce(t, op=rop, async_op=async_op)
+
+    def allreduce_scalar(self, v: float, op: str = "sum", device="cpu") -> float:
+        if self.size == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=device)
+        self.allreduce_(t, op)
+        return float(t.item())
+
+    def alltoallv(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits,
+                  async_op: bool = False):
+        if self.size == 1:
+            return None
+        return dist.all_to_all_single(out, inp, list(out_splits), list(in_splits),
+                                      async_op=async_op)
+
+    def barrier(self):
+        if self.size > 1:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[torch.cuda.current_device()])
+            else:
+                dist.barrier()
+
+    def gather_objects(self, obj):
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj)
+        return out
+
+
+def init_distributed(platform: str = "gpu", timeout_s: float = 600.0) -> Comm:
+    """Initialise the process group from the torchrun environment (if any)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if platform == "gpu" and torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if platform == "gpu" else "gloo"
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local_rank)
+        dist.init_process_group(**kw)
+    return Comm()
+
+
+def finalize() -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
