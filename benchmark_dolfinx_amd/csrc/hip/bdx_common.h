@@ -15,6 +15,8 @@
 constexpr int kMaxNd = 8;
 constexpr int kMaxNq = 9;
 
+enum { kGeomStored = 0, kGeomOTF = 1 };
+
 // 1D operator tables, passed by value as a kernel argument (< 1.5 KiB).
 template <typename T>
 struct OpTables {

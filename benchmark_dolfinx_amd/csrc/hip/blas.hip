@@ -150,6 +150,13 @@ extern "C" {
 
 int bdx_hip_partials_size() { return 2048; }
 
+// Fixed-order reduction of n per-block partials into out[slot].
+int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
+                        hipStream_t st) {
+  reduce_partials_kernel<<<1, kBlock, 0, st>>>(partials, n, out, slot);
+  return static_cast<int>(hipGetLastError());
+}
+
 #define BDX_BLAS_API(T, SUF)                                                  \
   int bdx_dot_##SUF(int64_t L1, int64_t ld, int64_t o0, int64_t o1, int64_t o2, \
                     const T* a, const T* b, double* partials, double* out,    \

@@ -1,0 +1,520 @@
+// Fused, atomic-free structured operator kernel ("fused", the fast path).
+//
+// Same operator as the reference's stiffness_operator_gpu
+// (src/laplacian_gpu.hpp:91-426) + geometry_computation_gpu
+// (src/geometry_gpu.hpp:26-132), re-designed for CDNA4:
+//
+// * Tiling.  A workgroup owns a tile of TY x TZ cells in the (y, z) plane and
+//   marches through all local cells along x.  Threads map to the tile's
+//   (cell, qy, qz) quadrature columns (TY*TZ*NQ^2 <= 256 lanes); each thread
+//   keeps its column's NQ values along x in registers, so every x-contraction
+//   is register-only and only the y/z contractions go through LDS.
+// * No atomics.  Cells of a layer scatter into an LDS dof slab in 4 parity
+//   phases (deterministic).  The x-shared dof plane is carried in LDS from one
+//   layer to the next.  Dofs on the tile's upper y/z faces (owned by the
+//   neighbouring tile) go to small interface buffers (YB, ZB, CB) that a light
+//   finalize kernel folds into y.  Every other dof is written exactly once,
+//   with a plain store, so y needs no zero fill.
+// * Geometry.  GEOM=otf recomputes J per quadrature point from the cell's 8
+//   vertices, exploiting the trilinear structure: dX/ds is constant along the
+//   thread's x column and dX/dt, dX/du are linear in s (6 FMAs per point),
+//   then F = kappa w/det adj(J) (adj(J)^T grad) without forming G.  GEOM=stored
+//   reads the reference-layout G[cell][6][nq^3] array (coalesced along z).
+// * CG fusion (MODE=1).  The input is formed on the fly as p = r + beta p_old
+//   (double-buffered p), written back once for tile-owned dofs, and the
+//   reduction p.(A p) is accumulated per cell (sum over the cell's dofs of
+//   p_i (A_c p)_i, exact because every cell is computed by exactly one
+//   rank/tile) plus p_i^2 for owned Dirichlet dofs (A has identity rows).
+//   So one CG iteration = this kernel + finalize + one fused x/r/r.r update.
+#pragma once
+#include "bdx_common.h"
+
+enum { kFusedAction = 0, kFusedCG = 1 };
+
+// Scheduling fence between unrolled iterations: keeps the scheduler from
+// hoisting every LDS read of a fully unrolled stage to its top (which costs
+// hundreds of registers and occupancy).
+// Pin values computed in an unrolled iteration before the next iteration's
+// LDS reads (the memory clobber keeps those reads below; the register
+// operands keep this iteration's FMAs above).  Without it the scheduler
+// issues every read of a stage first and spills the results.
+#define BDX_PIN1(x) asm volatile("" : "+v"(x)::"memory")
+#define BDX_PIN3(x, y, z) asm volatile("" : "+v"(x), "+v"(y), "+v"(z)::"memory")
+
+#ifndef BDX_NO_SCHED_FENCE
+#define BDX_SCHED_FENCE()               \
+  do {                                  \
+    asm volatile("" ::: "memory");      \
+    __builtin_amdgcn_sched_barrier(0);  \
+  } while (0)
+#else
+#define BDX_SCHED_FENCE()
+#endif
+
+#ifndef BDX_FUSED_WAVES
+#define BDX_FUSED_WAVES 1
+#endif
+
+template <int ND, int NQ, int TY, int TZ>
+struct FusedShape {
+  static constexpr int P = ND - 1;
+  static constexpr int cells = TY * TZ;
+  static constexpr int lanes = cells * NQ * NQ;
+  static constexpr int threads = ((lanes + 63) / 64) * 64;
+  static constexpr int DY = TY * P + 1;
+  static constexpr int DZ = TZ * P + 1;
+  static constexpr int slab = ND * DY * DZ;   // one layer's dof slab
+  static constexpr int work = cells * NQ * NQ * NQ;
+};
+
+// Tile selection per (ND, NQ): as many whole cells as fit in 256 lanes.
+template <int NQ> struct TileFor;
+template <> struct TileFor<2> { static constexpr int TY = 8, TZ = 8; };
+template <> struct TileFor<3> { static constexpr int TY = 4, TZ = 7; };
+template <> struct TileFor<4> { static constexpr int TY = 4, TZ = 4; };
+template <> struct TileFor<5> { static constexpr int TY = 2, TZ = 5; };
+template <> struct TileFor<6> { static constexpr int TY = 1, TZ = 7; };
+template <> struct TileFor<7> { static constexpr int TY = 1, TZ = 5; };
+template <> struct TileFor<8> { static constexpr int TY = 2, TZ = 2; };
+template <> struct TileFor<9> { static constexpr int TY = 1, TZ = 3; };
+
+template <typename T>
+struct FusedArgs {
+  BdxLattice lat;
+  const T* __restrict__ u;      // action: input; CG: r
+  const T* __restrict__ pold;   // CG: previous p (read)
+  T* __restrict__ pnew;         // CG: new p (written, tile-owned dofs)
+  T* __restrict__ y;            // output (tile-owned dofs)
+  T* __restrict__ yb;           // [Lx][nty-1][Lz]   upper-y face partials
+  T* __restrict__ zb;           // [Lx][Ly][ntz-1]   upper-z face partials
+  T* __restrict__ cb;           // [Lx][nty-1][ntz-1] upper corner partials
+  const T* __restrict__ G;      // stored geometry (GEOM=stored)
+  const T* __restrict__ xv;     // vertex coordinates (GEOM=otf)
+  const double* __restrict__ scal;
+  double* __restrict__ partials;  // per-block p.Ap
+  int beta_num, beta_den;       // CG: beta = scal[num]/scal[den]; num<0 -> beta=0
+  int nty, ntz;
+  T kappa;
+};
+
+template <typename T, int ND, int NQ, int TY, int TZ, int GEOM, int MODE>
+__global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUSED_WAVES)
+    lap_fused_kernel(FusedArgs<T> A, OpTables<T> tb) {
+  using S = FusedShape<ND, NQ, TY, TZ>;
+  constexpr int P = S::P, DY = S::DY, DZ = S::DZ;
+  constexpr int NQ2 = NQ * NQ;
+  constexpr bool IDENT = (ND == NQ);
+
+  __shared__ T s_phi[NQ * ND];       // phi0[q][i]
+  __shared__ T s_dphi[NQ * NQ];      // dphi1[q][j]
+  __shared__ T s_u[S::slab];         // input slab [ND][DY][DZ], BC dofs zeroed
+  __shared__ T s_y[S::slab];         // output slab
+  __shared__ T s_w1[S::work];        // [c][a][b][x] scratch
+  __shared__ T s_w2[S::work];
+  __shared__ T s_w3[S::work];
+  __shared__ T s_X[2][TY + 1][TZ + 1][3];  // vertex planes of the layer
+  __shared__ double s_red[16];
+  __shared__ T s_qw[2 * NQ];          // quadrature points, weights
+
+  const BdxLattice& lat = A.lat;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < NQ * ND; i += blockDim.x) s_phi[i] = tb.phi0[i];
+  for (int i = tid; i < NQ * NQ; i += blockDim.x) s_dphi[i] = tb.dphi1[i];
+  if (tid < NQ) {
+    s_qw[tid] = tb.qpts[tid];
+    s_qw[NQ + tid] = tb.wts[tid];
+  }
+
+  // XCD-aware bijective remap of the block id (tiles adjacent in z share an
+  // XCD's L2: cdna_hip_programming.md T1).
+  const int nblk = gridDim.x, ob = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
+  const int ty = bid / A.ntz, tz = bid % A.ntz;
+  const int64_t y0 = static_cast<int64_t>(ty) * TY * P, z0 = static_cast<int64_t>(tz) * TZ * P;
+  const int64_t Lx = lat.L[0], Ly = lat.L[1], Lz = lat.L[2];
+  const int64_t ncx = lat.n[0];
+  const bool top_y = (ty == A.nty - 1), top_z = (tz == A.ntz - 1);
+  // local dof extent of this tile's slab (clipped at the lattice end)
+  const int ey = static_cast<int>(y0 + DY <= Ly ? DY : Ly - y0);
+  const int ez = static_cast<int>(z0 + DZ <= Lz ? DZ : Lz - z0);
+  // tile-owned dof extents in y/z (the top tile owns the last plane)
+  const int oy = top_y ? ey : TY * P;
+  const int oz = top_z ? ez : TZ * P;
+
+  // thread -> (cell c = (cy, cz), a, b)
+  // idle lanes (tid >= lanes) alias the last cell for addressing only
+  const int c = (tid / NQ2 < S::cells) ? tid / NQ2 : S::cells - 1;
+  const int a = (tid / NQ) % NQ, b = tid % NQ;
+  const int cy = c / TZ, cz = c % TZ;
+  const bool lane_on = tid < S::lanes;
+  const bool cell_on = lane_on && (static_cast<int64_t>(ty) * TY + cy < lat.n[1]) &&
+                       (static_cast<int64_t>(tz) * TZ + cz < lat.n[2]);
+  const int yb = cy * P, zb = cz * P;
+  T* w1c = s_w1 + c * NQ * NQ2;
+  T* w2c = s_w2 + c * NQ * NQ2;
+  T* w3c = s_w3 + c * NQ * NQ2;
+
+  T beta = T(0);
+  if constexpr (MODE == kFusedCG) {
+    if (A.beta_num >= 0) beta = static_cast<T>(A.scal[A.beta_num] / A.scal[A.beta_den]);
+  }
+  double pap = 0.0;
+
+  auto gbc = [&](int64_t i, int64_t j, int64_t k) { return lat.is_bc(i, j, k); };
+
+  // Load dof planes [pl0, pl1) of layer cx into s_u (and write p, y for BC).
+  auto load_planes = [&](int64_t cx, int pl0, int pl1) {
+    const int n = (pl1 - pl0) * DY * DZ;
+    for (int e = tid; e < n; e += blockDim.x) {
+      const int pl = pl0 + e / (DY * DZ);
+      const int rem = e % (DY * DZ);
+      const int ly = rem / DZ, lz = rem % DZ;
+      const int64_t gx = cx * P + pl, gy = y0 + ly, gz = z0 + lz;
+      T v = T(0);
+      if (ly < ey && lz < ez) {
+        const int64_t id = lat.idx(gx, gy, gz);
+        if constexpr (MODE == kFusedCG) {
+          v = A.u[id] + beta * A.pold[id];
+        } else {
+          v = A.u[id];
+        }
+        const bool owned_tile = ly < oy && lz < oz;
+        if constexpr (MODE == kFusedCG) {
+          if (owned_tile) A.pnew[id] = v;
+        }
+        if (gbc(gx, gy, gz)) {
+          if (owned_tile) {
+            const bool rank_owned = lat.is_owned(gx, gy, gz);
+            A.y[id] = rank_owned ? v : T(0);
+            if constexpr (MODE == kFusedCG) {
+              if (rank_owned) pap += static_cast<double>(v) * static_cast<double>(v);
+            }
+          }
+          v = T(0);
+        }
+      }
+      s_u[(pl * DY + ly) * DZ + lz] = v;
+    }
+  };
+
+  // Per-thread vertex-derived geometry coefficients for the current layer.
+  T Js[3] = {0, 0, 0};                 // dX/ds at (t_a, u_b): constant in s
+  T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};  // dX/dt = Jt0 + s (Jt1 - Jt0)
+  T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};  // dX/du = Ju0 + s (Ju1 - Ju0)
+
+  // ---- prologue: first layer's planes and carry init
+  for (int e = tid; e < S::slab; e += blockDim.x) s_y[e] = T(0);
+  load_planes(0, 0, ND);
+
+  for (int64_t cx = 0; cx < ncx; ++cx) {
+    // Opaque zero: stops the compiler hoisting the 1D-table reads out of the
+    // x-march (they would pin ~2*(NQ^2 + NQ*ND) registers for the whole loop).
+    int toff = 0;
+    asm volatile("" : "+s"(toff));
+    const T* __restrict__ Dm = s_dphi + toff;  // dphi1[q][m]
+    const T* __restrict__ Ph = s_phi + toff;   // phi0[q][i]
+    if constexpr (GEOM == kGeomOTF) {
+      // vertex planes x = cx, cx+1 of the tile
+      constexpr int nv = 2 * (TY + 1) * (TZ + 1) * 3;
+      for (int e = tid; e < nv; e += blockDim.x) {
+        const int d = e % 3, r = e / 3;
+        const int vz = r % (TZ + 1), vy = (r / (TZ + 1)) % (TY + 1), vx = r / ((TY + 1) * (TZ + 1));
+        const int64_t gy = static_cast<int64_t>(ty) * TY + vy, gz = static_cast<int64_t>(tz) * TZ + vz;
+        T val = T(0);
+        if (gy <= lat.n[1] && gz <= lat.n[2]) val = A.xv[3 * lat.vidx(cx + vx, gy, gz) + d];
+        s_X[vx][vy][vz][d] = val;
+      }
+    }
+    __syncthreads();
+
+    // ------------------------------------------------ interpolate to qpts
+    // per-thread LDS bases: every access below is base + compile-time offset
+    const T* __restrict__ ua = s_u + (yb + a) * DZ + zb;
+    T* __restrict__ w1ab = w1c + (a * NQ + b) * NQ;
+    T* __restrict__ w2ab = w2c + (a * NQ + b) * NQ;
+    T* __restrict__ w3ab = w3c + (a * NQ + b) * NQ;
+    const T* __restrict__ w1b = w1c + b * NQ;
+    const T* __restrict__ w2b = w2c + b * NQ;
+    const T* __restrict__ w1a = w1c + a * NQ2;
+    const T* __restrict__ w2a = w2c + a * NQ2;
+    const T* __restrict__ w3a = w3c + a * NQ2;
+    const T* __restrict__ Dma = Dm + a * NQ;   // dphi1[a][.]
+    const T* __restrict__ Dmb = Dm + b * NQ;   // dphi1[b][.]
+    const T* __restrict__ DmTa = Dm + a;       // dphi1[.][a]
+    const T* __restrict__ DmTb = Dm + b;       // dphi1[.][b]
+
+    T U[NQ];
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int i = 0; i < NQ; ++i)
+        U[i] = lane_on ? ua[i * DY * DZ + b] : T(0);
+    } else {
+      // S1: z-interp, thread (c, a=j<ND, b=qz): w1[a][b][i]
+      if (lane_on && a < ND) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+          T acc = 0;
+#pragma unroll
+          for (int k = 0; k < ND; ++k) acc += Ph[b * ND + k] * ua[i * DY * DZ + k];
+          w1ab[i] = acc;
+        }
+      }
+      __syncthreads();
+      // S2: y-interp, thread (c, a=qy, b=qz)
+      T t2[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        T acc = 0;
+#pragma unroll
+        for (int j = 0; j < ND; ++j) acc += Ph[a * ND + j] * w1b[j * NQ2 + i];
+        t2[i] = lane_on ? acc : T(0);
+      }
+      // S3: x-interp in registers
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        T acc = 0;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) acc += Ph[q * ND + i] * t2[i];
+        U[q] = acc;
+      }
+    }
+
+    // ------------------------------------------------ geometry coefficients
+    if constexpr (GEOM == kGeomOTF) {
+      // bilinear coefficients of this column (cell (cy, cz), point (t_a, u_b))
+      const T t = s_qw[a], u = s_qw[b];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const T X000 = s_X[0][cy][cz][d], X001 = s_X[0][cy][cz + 1][d];
+        const T X010 = s_X[0][cy + 1][cz][d], X011 = s_X[0][cy + 1][cz + 1][d];
+        const T X100 = s_X[1][cy][cz][d], X101 = s_X[1][cy][cz + 1][d];
+        const T X110 = s_X[1][cy + 1][cz][d], X111 = s_X[1][cy + 1][cz + 1][d];
+        Js[d] = (1 - t) * ((1 - u) * (X100 - X000) + u * (X101 - X001)) +
+                t * ((1 - u) * (X110 - X010) + u * (X111 - X011));
+        Jt0[d] = (1 - u) * (X010 - X000) + u * (X011 - X001);
+        Jt1[d] = (1 - u) * (X110 - X100) + u * (X111 - X101) - Jt0[d];
+        Ju0[d] = (1 - t) * (X001 - X000) + t * (X011 - X010);
+        Ju1[d] = (1 - t) * (X101 - X100) + t * (X111 - X110) - Ju0[d];
+      }
+    }
+    const T kwyz = A.kappa * s_qw[NQ + a] * s_qw[NQ + b];
+    int64_t gcell = 0;
+    if constexpr (GEOM == kGeomStored) {
+      gcell = ((cx * lat.n[1] + static_cast<int64_t>(ty) * TY + cy) * lat.n[2] +
+               static_cast<int64_t>(tz) * TZ + cz) * 6 * (NQ * NQ2) + a * NQ + b;
+    }
+
+    // ------------------------------------------------ gradient -> F (streamed over x)
+    if (lane_on) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) w2ab[q] = U[q];
+    }
+    __syncthreads();
+    T Fx[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      BDX_SCHED_FENCE();
+      T gx = 0, gy = 0, gz = 0;
+#pragma unroll
+      for (int m = 0; m < NQ; ++m) {
+        gx += Dm[q * NQ + m] * U[m];
+        gy += Dma[m] * w2b[m * NQ2 + q];
+        gz += Dmb[m] * w2a[m * NQ + q];
+      }
+      T fx, fy, fz;
+      if constexpr (GEOM == kGeomOTF) {
+        const T s = tb.qpts[q];
+        const T J00 = Js[0], J10 = Js[1], J20 = Js[2];
+        const T J01 = Jt0[0] + s * Jt1[0], J11 = Jt0[1] + s * Jt1[1], J21 = Jt0[2] + s * Jt1[2];
+        const T J02 = Ju0[0] + s * Ju1[0], J12 = Ju0[1] + s * Ju1[1], J22 = Ju0[2] + s * Ju1[2];
+        // K = adj(J)
+        const T K00 = J11 * J22 - J12 * J21, K01 = J02 * J21 - J01 * J22, K02 = J01 * J12 - J02 * J11;
+        const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
+        const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
+        const T det = J00 * K00 + J01 * K10 + J02 * K20;
+        const T sc = kwyz * tb.wts[q] / det;
+        // h = K^T g, F = sc K h  (= kappa w det J^-1 J^-T g)
+        const T h0 = K00 * gx + K10 * gy + K20 * gz;
+        const T h1 = K01 * gx + K11 * gy + K21 * gz;
+        const T h2 = K02 * gx + K12 * gy + K22 * gz;
+        fx = sc * (K00 * h0 + K01 * h1 + K02 * h2);
+        fy = sc * (K10 * h0 + K11 * h1 + K12 * h2);
+        fz = sc * (K20 * h0 + K21 * h1 + K22 * h2);
+      } else {
+        T Gd[6] = {0, 0, 0, 0, 0, 0};
+        if (cell_on) {
+          const T* g = A.G + gcell + q * NQ2;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) Gd[k] = __builtin_nontemporal_load(g + k * NQ * NQ2);
+        }
+        fx = A.kappa * (Gd[0] * gx + Gd[1] * gy + Gd[2] * gz);
+        fy = A.kappa * (Gd[1] * gx + Gd[3] * gy + Gd[4] * gz);
+        fz = A.kappa * (Gd[2] * gx + Gd[4] * gy + Gd[5] * gz);
+      }
+      BDX_PIN3(fx, fy, fz);
+      Fx[q] = fx;
+      if (lane_on) {
+        w1ab[q] = fy;
+        w3ab[q] = fz;
+      }
+    }
+    __syncthreads();
+
+    // ------------------------------------------------ transposed gradient (+ x interp^T)
+    T sx[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) sx[i] = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      BDX_SCHED_FENCE();
+      T acc = 0;
+#pragma unroll
+      for (int m = 0; m < NQ; ++m) {
+        acc += Dm[m * NQ + q] * Fx[m];
+        acc += DmTa[m * NQ] * w1b[m * NQ2 + q];
+        acc += DmTb[m * NQ] * w3a[m * NQ + q];
+      }
+      BDX_PIN1(acc);
+      if constexpr (IDENT) {
+        sx[q] = acc;
+      } else {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) sx[i] += Ph[q * ND + i] * acc;
+      }
+    }
+
+    // ------------------------------------------------ back to the dofs
+    T ye[ND];
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) ye[i] = sx[i];
+    } else {
+      __syncthreads();  // reads of w1/w3 done
+      if (lane_on) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) w2ab[i] = sx[i];
+      }
+      __syncthreads();
+      // S8: y, thread (c, a=j<ND, b=qz)
+      if (lane_on && a < ND) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+          T acc = 0;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) acc += Ph[q * ND + a] * w2b[q * NQ2 + i];
+          w1ab[i] = acc;
+        }
+      }
+      __syncthreads();
+      // S9: z, thread (c, a=j<ND, b=k<ND)
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        T acc = 0;
+        if (a < ND && b < ND) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) acc += Ph[q * ND + b] * w1a[q * NQ + i];
+        }
+        ye[i] = acc;
+      }
+    }
+
+    // ------------------------------------------------ scatter into the slab
+    const bool dof_lane = cell_on && a < ND && b < ND;
+    if constexpr (MODE == kFusedCG) {
+      if (dof_lane) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          pap += static_cast<double>(ua[i * DY * DZ + b]) * static_cast<double>(ye[i]);
+      }
+    }
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      if (dof_lane && ((cy & 1) * 2 + (cz & 1)) == ph) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) s_y[(yb + a) * DZ + zb + b + i * DY * DZ] += ye[i];
+      }
+      __syncthreads();
+    }
+
+    // ------------------------------------------------ write out the layer
+    const bool last = (cx == ncx - 1);
+    const int npl = last ? ND : P;
+    {
+      const int n = npl * DY * DZ;
+      for (int e = tid; e < n; e += blockDim.x) {
+        const int pl = e / (DY * DZ);
+        const int rem = e % (DY * DZ);
+        const int ly = rem / DZ, lz = rem % DZ;
+        if (ly >= ey || lz >= ez) continue;
+        const int64_t gx = cx * P + pl, gy = y0 + ly, gz = z0 + lz;
+        const bool bc = gbc(gx, gy, gz);
+        const T v = bc ? T(0) : s_y[e];
+        const bool iy = ly < oy, iz = lz < oz;
+        if (iy && iz) {
+          if (!bc) A.y[lat.idx(gx, gy, gz)] = v;
+        } else if (!iy && iz) {
+          A.yb[(gx * (A.nty - 1) + ty) * Lz + gz] = v;
+        } else if (iy && !iz) {
+          A.zb[(gx * Ly + gy) * (A.ntz - 1) + tz] = v;
+        } else {
+          A.cb[(gx * (A.nty - 1) + ty) * (A.ntz - 1) + tz] = v;
+        }
+      }
+    }
+    if (!last) {
+      __syncthreads();
+      // carry plane P -> plane 0, clear the others; shift the input slab
+      for (int e = tid; e < DY * DZ; e += blockDim.x) {
+        s_y[e] = s_y[P * DY * DZ + e];
+        s_u[e] = s_u[P * DY * DZ + e];
+      }
+      for (int e = tid; e < P * DY * DZ; e += blockDim.x) s_y[DY * DZ + e] = T(0);
+      __syncthreads();
+      load_planes(cx + 1, 1, ND);
+    }
+  }
+  (void)Lx;
+  if constexpr (MODE == kFusedCG) {
+    const double t = block_sum(pap, s_red);
+    if (tid == 0) A.partials[blockIdx.x] = t;
+  }
+}
+
+// Fold the interface partials into y (all local dofs incl. ghost planes).
+// Index space: [YB rows: Lx * (nty-1) * Lz] ++ [ZB columns not on a YB row:
+// Lx * Ly * (ntz-1)].  The two dof sets are disjoint, so no races.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    fused_finalize_kernel(BdxLattice lat, T* __restrict__ y, const T* __restrict__ yb,
+                          const T* __restrict__ zb, const T* __restrict__ cb, int nty,
+                          int ntz, int sy, int sz) {
+  const int64_t Lx = lat.L[0], Ly = lat.L[1], Lz = lat.L[2];
+  const int64_t n1 = Lx * (nty - 1) * Lz;
+  const int64_t n2 = Lx * Ly * (ntz - 1);
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n1 + n2;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    if (t < n1) {
+      const int64_t z = t % Lz;
+      const int64_t r = t / Lz;
+      const int64_t tym1 = r % (nty - 1), x = r / (nty - 1);
+      const int64_t yy = (tym1 + 1) * sy;
+      T add = yb[t];
+      const int64_t tzz = z / sz;
+      if (z % sz == 0 && tzz >= 1 && tzz < ntz) {
+        add += zb[(x * Ly + yy) * (ntz - 1) + (tzz - 1)];
+        add += cb[(x * (nty - 1) + tym1) * (ntz - 1) + (tzz - 1)];
+      }
+      y[lat.idx(x, yy, z)] += add;
+    } else {
+      const int64_t s = t - n1;
+      const int64_t tzm1 = s % (ntz - 1);
+      const int64_t r = s / (ntz - 1);
+      const int64_t yy = r % Ly, x = r / Ly;
+      const int64_t tyy = yy / sy;
+      if (yy % sy == 0 && tyy >= 1 && tyy < nty) continue;  // handled by the YB pass
+      const int64_t z = (tzm1 + 1) * sz;
+      y[lat.idx(x, yy, z)] += zb[s];
+    }
+  }
+}

@@ -17,7 +17,7 @@
 #include "bdx_common.h"
 
 enum { kModeStiffness = 0, kModeMass = 1 };
-enum { kGeomStored = 0, kGeomOTF = 1 };
+
 
 // Cell index of the reference-layout G array: lexicographic over the local box.
 __device__ __forceinline__ int64_t cell_index(const BdxLattice& lat, int64_t cx,

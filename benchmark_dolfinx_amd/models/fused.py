@@ -1,0 +1,120 @@
+"""Fused structured GPU operator (the fast path; csrc/hip/lap_fused.h).
+
+Operator semantics are those of `MatFreeLaplacianGPU` (reference
+MatFreeLaplacianGPU, src/laplacian.hpp:87-448) but the whole CG iteration
+is restructured around one kernel (see lap_fused.h for the design):
+
+  iteration k:  [halo fwd of r]  fused(p = r + beta p_old, y = A p, p.y partials)
+                -> finalize (fold tile-interface partials into y)
+                -> [halo rev of y] -> reduce p.y -> [all-reduce]
+                -> x += a p, r -= a y, r.r -> [all-reduce]
+
+versus the reference's fill + pack/unpack x2 + 2 stiffness launches + 2
+Thrust reductions (host round trips) + 3 axpy launches.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from ..ops import native
+from ..ops.kernels import _check, _stream
+from ..ops.native import ptr
+from ..utils.timing import timed
+
+
+def fused_supported(pb) -> bool:
+    if pb.platform != "gpu":
+        return False
+    lib = native.hip()
+    return hasattr(lib, f"bdx_fused_apply_{pb.suf}_p{pb.degree}")
+
+
+class FusedLaplacianGPU:
+    name = "fused"
+
+    def __init__(self, pb, geometry: str = "otf"):
+        if geometry not in ("otf", "stored"):
+            raise ValueError(f"unknown geometry mode {geometry}")
+        self.pb = pb
+        self.geometry = geometry
+        self.lib = native.hip()
+        lat = pb.lat
+        t = pb.kernels.t
+        self.t = t
+        ty, tz = ctypes.c_int(0), ctypes.c_int(0)
+        _check(self.lib.bdx_fused_tile(t.nq, ctypes.byref(ty), ctypes.byref(tz)), "fused_tile")
+        self.TY, self.TZ = ty.value, tz.value
+        P = lat.degree
+        self.nty = max(1, math.ceil(lat.n[1] / self.TY))
+        self.ntz = max(1, math.ceil(lat.n[2] / self.TZ))
+        self.sy, self.sz = self.TY * P, self.TZ * P
+        Lx, Ly, Lz = lat.L
+        dev, dt = pb.device, pb.dtype
+        self.yb = torch.zeros(max(1, Lx * (self.nty - 1) * Lz), dtype=dt, device=dev)
+        self.zb = torch.zeros(max(1, Lx * Ly * (self.ntz - 1)), dtype=dt, device=dev)
+        self.cb = torch.zeros(max(1, Lx * (self.nty - 1) * (self.ntz - 1)), dtype=dt, device=dev)
+        self.nblocks = self.nty * self.ntz
+        self.partials = torch.zeros(self.nblocks, dtype=torch.float64, device=dev)
+        self.G = None
+        if geometry == "stored":
+            with timed("~setup geometry"):
+                self.G = torch.empty(lat.ncells_local * 6 * t.nq ** 3, dtype=dt, device=dev)
+                pb.kernels.geometry(pb.xv, self.G)
+        self._apply = getattr(self.lib, f"bdx_fused_apply_{pb.suf}_p{P}")
+        self._final = getattr(self.lib, f"bdx_fused_finalize_{pb.suf}")
+        self.geom_code = 1 if geometry == "otf" else 0
+        self.p_old = None
+        self.p_new = None
+
+    # ------------------------------------------------------------ launches
+    def _launch(self, mode, u, pold, pnew, y, scal=None, beta_num=-1, beta_den=-1):
+        pb, t = self.pb, self.t
+        _check(self._apply(self.geom_code, mode, ptr(pb.latd), t.nq, ptr(t.phi0), ptr(t.dphi1),
+                           ptr(t.wts), ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(y),
+                           ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(self.G), ptr(pb.xv),
+                           pb.kappa, ptr(scal), ptr(self.partials), beta_num, beta_den,
+                           self.nty, self.ntz, _stream()), "fused_apply")
+        _check(self._final(ptr(pb.latd), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
+                           self.nty, self.ntz, self.sy, self.sz, _stream()), "fused_finalize")
+
+    def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
+        """y = A u (action mode)."""
+        halo = self.pb.halo
+        halo.forward(u)
+        self._launch(0, u, None, None, y)
+        halo.reverse(y)
+
+    # ------------------------------------------------------------- CG
+    def cg_start(self, cg, x, b):
+        k, r, y = cg.k, cg.r, cg.y
+        self.apply(x, y)
+        k.axpy(r, -1.0, y, b)
+        k.dot(r, r, cg.partials, cg.scal, cg.RR0)
+        cg._allreduce(cg.RR0)
+        if self.p_old is None:
+            self.p_old = self.pb.new_vector()
+            self.p_new = self.pb.new_vector()
+        else:
+            self.p_old.zero_()
+
+    def cg_iterate(self, cg, n):
+        k, r, y, x, scal = cg.k, cg.r, cg.y, cg.x, cg.scal
+        halo = self.pb.halo
+        for _ in range(n):
+            cur = cg.RR0 if cg.it % 2 == 0 else cg.RR1
+            nxt = cg.RR1 if cg.it % 2 == 0 else cg.RR0
+            halo.forward(r)
+            bnum, bden = (cur, nxt) if cg.it > 0 else (-1, -1)
+            self._launch(1, r, self.p_old, self.p_new, y, scal, bnum, bden)
+            halo.reverse(y)
+            _check(self.lib.bdx_reduce_partials(ptr(self.partials), self.nblocks, ptr(scal),
+                                                cg.PAP, _stream()), "reduce_partials")
+            cg._allreduce(cg.PAP)
+            k.cg_update(x, r, self.p_new, y, scal, cur, cg.PAP, nxt, cg.partials)
+            cg._allreduce(nxt)
+            self.p_old, self.p_new = self.p_new, self.p_old
+            cg.it += 1

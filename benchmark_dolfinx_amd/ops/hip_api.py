@@ -32,8 +32,12 @@ def declare(lib) -> None:
            [i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp])
         _d(lib, f"bdx_geometry_{suf}", [vp, i32, vp, vp, vp, vp, vp, vp, vp])
         _d(lib, f"bdx_spmv_{suf}", [i64, vp, vp, vp, vp, vp, vp])
-        if hasattr(lib, f"bdx_fused_apply_{suf}"):
-            _d(lib, f"bdx_fused_apply_{suf}",
-               [i32, vp, i32, vp, vp, vp, vp, i32, vp, f64, vp, vp, vp, vp, vp,
-                vp, i32, i32, vp, vp, vp])
+        for P in range(1, 8):
+            name = f"bdx_fused_apply_{suf}_p{P}"
+            if hasattr(lib, name):
+                _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                               vp, vp, vp, f64, vp, vp, i32, i32, i32, i32, vp])
+        _d(lib, f"bdx_fused_finalize_{suf}", [vp, vp, vp, vp, vp, i32, i32, i32, i32, vp])
+    _d(lib, "bdx_fused_tile", [i32, vp, vp])
+    _d(lib, "bdx_reduce_partials", [vp, i32, vp, i32, vp])
     del ft

@@ -69,6 +69,117 @@ class Comm:
         return out
 
 
+class _Done:
+    def wait(self):
+        return None
+
+
+class ThreadGroup:
+    """Shared state of an in-process group of ranks (one Python thread each)."""
+
+    def __init__(self, size: int):
+        import threading
+        self.size = size
+        self.barrier = threading.Barrier(size)
+        self.slots = [None] * size
+
+
+class ThreadComm(Comm):
+    """Rank of an in-process thread group.
+
+    Lets tests (and rehearsals) run R ranks of the real code path in one
+    process -- on the CPU, or on ONE GPU with the HIP kernels (RCCL cannot put
+    two ranks on one device).  Collectives are executed with tensor copies on
+    the device's default stream, ordered by the group barrier; reductions sum
+    in rank order, so results are deterministic.
+    """
+
+    def __init__(self, group: ThreadGroup, rank: int):
+        self.enabled = True
+        self.rank = rank
+        self.size = group.size
+        self.backend = "thread"
+        self.g = group
+
+    def _sync_dev(self, t):
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            torch.cuda.synchronize(t.device)
+
+    def allreduce_(self, t, op: str = "sum", async_op: bool = False):
+        if self.size == 1:
+            return _Done() if async_op else None
+        self.g.slots[self.rank] = t.detach().clone()
+        self._sync_dev(t)
+        self.g.barrier.wait()
+        vals = [s.to(t.device) for s in self.g.slots]
+        acc = vals[0].clone()
+        for v in vals[1:]:
+            if op == "sum":
+                acc += v
+            elif op == "max":
+                acc = torch.maximum(acc, v)
+            else:
+                acc = torch.minimum(acc, v)
+        self._sync_dev(acc)
+        self.g.barrier.wait()
+        t.copy_(acc)
+        self._sync_dev(t)
+        return _Done() if async_op else None
+
+    def alltoallv(self, out, inp, out_splits, in_splits, async_op: bool = False):
+        if self.size == 1:
+            return _Done() if async_op else None
+        self._sync_dev(inp)
+        self.g.slots[self.rank] = (inp, list(in_splits))
+        self.g.barrier.wait()
+        off_out = 0
+        for p in range(self.size):
+            pin, psplits = self.g.slots[p]
+            n = psplits[self.rank]
+            assert n == out_splits[p], (n, out_splits[p])
+            if n:
+                o = sum(psplits[: self.rank])
+                out[off_out: off_out + n].copy_(pin[o: o + n].to(out.device))
+            off_out += out_splits[p]
+        self._sync_dev(out)
+        self.g.barrier.wait()
+        return _Done() if async_op else None
+
+    def barrier(self):
+        self.g.barrier.wait()
+
+    def gather_objects(self, obj):
+        self.g.slots[self.rank] = obj
+        self.g.barrier.wait()
+        out = list(self.g.slots)
+        self.g.barrier.wait()
+        return out
+
+
+def run_threaded(size: int, fn, *args, **kwargs):
+    """Run fn(comm, *args) on `size` in-process ranks; returns the per-rank results."""
+    import threading
+    group = ThreadGroup(size)
+    results = [None] * size
+    errors = []
+
+    def body(r):
+        try:
+            results[r] = fn(ThreadComm(group, r), *args, **kwargs)
+        except BaseException as e:  # pragma: no cover - re-raised below
+            errors.append(e)
+            group.barrier.abort()
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(size)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errors:
+        raise errors[0]
+    return results
+
+
 def init_distributed(platform: str = "gpu", timeout_s: float = 600.0) -> Comm:
     """Initialise the process group from the torchrun environment (if any)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -13,8 +13,8 @@ p0 = r0, rtol = 0 runs exactly max_iter iterations):
   One halo exchange per iteration (the reference does two, quirk Q2) and no
   host synchronisation (quirk Q3).
 
-When the operator provides `cg_iteration` (the fused structured kernel,
-models/fused.py) the device loop delegates to it.
+When the operator provides `cg_start` / `cg_iterate` (the fused structured
+kernel, models/fused.py) the device loop delegates to it.
 """
 
 from __future__ import annotations
@@ -68,25 +68,45 @@ class DeviceCG:
         if self.pb.comm.size > 1:
             self.pb.comm.allreduce_(self.scal[slot: slot + 1])
 
-    def solve(self, op, x: torch.Tensor, b: torch.Tensor, max_iter: int) -> int:
-        if hasattr(op, "cg_solve"):
-            return op.cg_solve(self, x, b, max_iter)
+    def start(self, op, x: torch.Tensor, b: torch.Tensor) -> None:
+        """r0 = b - A x0, p0 = r0, rho0 = p0.r0 (the prologue of src/cg.hpp:98-112)."""
+        self.op, self.x, self.it = op, x, 0
+        if hasattr(op, "cg_start"):
+            op.cg_start(self, x, b)
+            return
         k, r, y, p, scal = self.k, self.r, self.y, self.p, self.scal
         op.apply(x, y)
-        k.axpy(r, -1.0, y, b)          # r = b - A x0
+        k.axpy(r, -1.0, y, b)
         p.copy_(r)
         k.dot(p, r, self.partials, scal, self.RR0)
         self._allreduce(self.RR0)
-        for it in range(max_iter):
-            cur = self.RR0 if it % 2 == 0 else self.RR1
-            nxt = self.RR1 if it % 2 == 0 else self.RR0
+
+    def iterate(self, n: int) -> None:
+        """Run n CG iterations (state persists across calls)."""
+        op, x = self.op, self.x
+        if hasattr(op, "cg_iterate"):
+            op.cg_iterate(self, n)
+            return
+        k, r, y, p, scal = self.k, self.r, self.y, self.p, self.scal
+        for _ in range(n):
+            cur = self.RR0 if self.it % 2 == 0 else self.RR1
+            nxt = self.RR1 if self.it % 2 == 0 else self.RR0
             op.apply(p, y)
             k.dot(p, y, self.partials, scal, self.PAP)
             self._allreduce(self.PAP)
             k.cg_update(x, r, p, y, scal, cur, self.PAP, nxt, self.partials)
             self._allreduce(nxt)
             k.p_update(p, r, scal, nxt, cur)
+            self.it += 1
+
+    def solve(self, op, x: torch.Tensor, b: torch.Tensor, max_iter: int) -> int:
+        self.start(op, x, b)
+        self.iterate(max_iter)
         return max_iter
+
+    def residual_norm2(self) -> float:
+        slot = self.RR0 if self.it % 2 == 0 else self.RR1
+        return float(self.scal[slot].item())
 
 
 def cg_solve_device(op, pb, x: torch.Tensor, b: torch.Tensor, max_iter: int) -> int:
