@@ -101,25 +101,29 @@ template <typename T, int ND, int NQ, int TY, int TZ, int GEOM, int MODE>
 __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUSED_WAVES)
     lap_fused_kernel(FusedArgs<T> A, OpTables<T> tb) {
   using S = FusedShape<ND, NQ, TY, TZ>;
-  constexpr int P = S::P, DY = S::DY, DZ = S::DZ;
+  constexpr int P = S::P, DY = S::DY, DZ = S::DZ, PL = DY * DZ;
   constexpr int NQ2 = NQ * NQ;
   constexpr bool IDENT = (ND == NQ);
+  constexpr int NT = S::threads;
+  constexpr int NPF = (P * PL + NT - 1) / NT;          // prefetched dofs per thread
+  constexpr int NV = (TY + 1) * (TZ + 1) * 3;          // vertex values per plane
+  constexpr int NPV = (NV + NT - 1) / NT;
 
-  __shared__ T s_phi[NQ * ND];       // phi0[q][i]
-  __shared__ T s_dphi[NQ * NQ];      // dphi1[q][j]
-  __shared__ T s_u[S::slab];         // input slab [ND][DY][DZ], BC dofs zeroed
-  __shared__ T s_y[S::slab];         // output slab
-  __shared__ T s_w1[S::work];        // [c][a][b][x] scratch
+  __shared__ T s_phi[NQ * ND];        // phi0[q][i]
+  __shared__ T s_dphi[NQ * NQ];       // dphi1[q][j]
+  __shared__ T s_qw[2 * NQ];          // quadrature points, weights
+  __shared__ T s_u[2][ND * PL];       // input slab [pl][ly][lz] (BC dofs zeroed), double-buffered
+  __shared__ T s_c[2][PL];            // x-carried output plane, ping-pong
+  __shared__ T s_w1[S::work];         // [c][a][b][x] scratch
   __shared__ T s_w2[S::work];
   __shared__ T s_w3[S::work];
-  __shared__ T s_X[2][TY + 1][TZ + 1][3];  // vertex planes of the layer
+  __shared__ T s_X[2][2 * NV];        // vertex planes (cx, cx+1) of the tile, double-buffered
   __shared__ double s_red[16];
-  __shared__ T s_qw[2 * NQ];          // quadrature points, weights
 
   const BdxLattice& lat = A.lat;
   const int tid = threadIdx.x;
-  for (int i = tid; i < NQ * ND; i += blockDim.x) s_phi[i] = tb.phi0[i];
-  for (int i = tid; i < NQ * NQ; i += blockDim.x) s_dphi[i] = tb.dphi1[i];
+  for (int i = tid; i < NQ * ND; i += NT) s_phi[i] = tb.phi0[i];
+  for (int i = tid; i < NQ * NQ; i += NT) s_dphi[i] = tb.dphi1[i];
   if (tid < NQ) {
     s_qw[tid] = tb.qpts[tid];
     s_qw[NQ + tid] = tb.wts[tid];
@@ -132,7 +136,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
   const int ty = bid / A.ntz, tz = bid % A.ntz;
   const int64_t y0 = static_cast<int64_t>(ty) * TY * P, z0 = static_cast<int64_t>(tz) * TZ * P;
-  const int64_t Lx = lat.L[0], Ly = lat.L[1], Lz = lat.L[2];
+  const int64_t Ly = lat.L[1], Lz = lat.L[2];
   const int64_t ncx = lat.n[0];
   const bool top_y = (ty == A.nty - 1), top_z = (tz == A.ntz - 1);
   // local dof extent of this tile's slab (clipped at the lattice end)
@@ -142,8 +146,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
   const int oy = top_y ? ey : TY * P;
   const int oz = top_z ? ez : TZ * P;
 
-  // thread -> (cell c = (cy, cz), a, b)
-  // idle lanes (tid >= lanes) alias the last cell for addressing only
+  // thread -> (cell c = (cy, cz), a, b); idle lanes alias the last cell
   const int c = (tid / NQ2 < S::cells) ? tid / NQ2 : S::cells - 1;
   const int a = (tid / NQ) % NQ, b = tid % NQ;
   const int cy = c / TZ, cz = c % TZ;
@@ -161,76 +164,103 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
   }
   double pap = 0.0;
 
-  auto gbc = [&](int64_t i, int64_t j, int64_t k) { return lat.is_bc(i, j, k); };
-
-  // Load dof planes [pl0, pl1) of layer cx into s_u (and write p, y for BC).
-  auto load_planes = [&](int64_t cx, int pl0, int pl1) {
-    const int n = (pl1 - pl0) * DY * DZ;
-    for (int e = tid; e < n; e += blockDim.x) {
-      const int pl = pl0 + e / (DY * DZ);
-      const int rem = e % (DY * DZ);
-      const int ly = rem / DZ, lz = rem % DZ;
-      const int64_t gx = cx * P + pl, gy = y0 + ly, gz = z0 + lz;
-      T v = T(0);
-      if (ly < ey && lz < ez) {
-        const int64_t id = lat.idx(gx, gy, gz);
+  // Input value of dof (gx, ly, lz) for the slab; side effects for CG (write
+  // p) and for Dirichlet dofs (y = p on the owner, p^2 into p.Ap).
+  auto stage = [&](int64_t gx, int ly, int lz, T r, T po) -> T {
+    const int64_t gy = y0 + ly, gz = z0 + lz;
+    const int64_t id = lat.idx(gx, gy, gz);
+    T v;
+    if constexpr (MODE == kFusedCG) {
+      v = r + beta * po;
+    } else {
+      v = r;
+      (void)po;
+    }
+    const bool owned_tile = ly < oy && lz < oz;
+    if constexpr (MODE == kFusedCG) {
+      if (owned_tile) A.pnew[id] = v;
+    }
+    if (lat.is_bc(gx, gy, gz)) {
+      if (owned_tile) {
+        const bool rank_owned = lat.is_owned(gx, gy, gz);
+        A.y[id] = rank_owned ? v : T(0);
         if constexpr (MODE == kFusedCG) {
-          v = A.u[id] + beta * A.pold[id];
-        } else {
-          v = A.u[id];
-        }
-        const bool owned_tile = ly < oy && lz < oz;
-        if constexpr (MODE == kFusedCG) {
-          if (owned_tile) A.pnew[id] = v;
-        }
-        if (gbc(gx, gy, gz)) {
-          if (owned_tile) {
-            const bool rank_owned = lat.is_owned(gx, gy, gz);
-            A.y[id] = rank_owned ? v : T(0);
-            if constexpr (MODE == kFusedCG) {
-              if (rank_owned) pap += static_cast<double>(v) * static_cast<double>(v);
-            }
-          }
-          v = T(0);
+          if (rank_owned) pap += static_cast<double>(v) * static_cast<double>(v);
         }
       }
-      s_u[(pl * DY + ly) * DZ + lz] = v;
+      v = T(0);
     }
+    return v;
+  };
+  auto vertex = [&](int64_t vx, int e) -> T {
+    const int d = e % 3, r = e / 3;
+    const int vz = r % (TZ + 1), vy = r / (TZ + 1);
+    const int64_t gy = static_cast<int64_t>(ty) * TY + vy, gz = static_cast<int64_t>(tz) * TZ + vz;
+    if (gy > lat.n[1] || gz > lat.n[2]) return T(0);
+    return A.xv[3 * lat.vidx(vx, gy, gz) + d];
   };
 
-  // Per-thread vertex-derived geometry coefficients for the current layer.
-  T Js[3] = {0, 0, 0};                 // dX/ds at (t_a, u_b): constant in s
-  T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};  // dX/dt = Jt0 + s (Jt1 - Jt0)
-  T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};  // dX/du = Ju0 + s (Ju1 - Ju0)
+  // ---- prologue: layer 0 input planes, vertex planes 0/1, zero carry
+  for (int e = tid; e < ND * PL; e += NT) {
+    const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+    T v = T(0);
+    if (ly < ey && lz < ez) {
+      const int64_t id = lat.idx(pl, y0 + ly, z0 + lz);
+      v = stage(pl, ly, lz, A.u[id], MODE == kFusedCG ? A.pold[id] : T(0));
+    }
+    s_u[0][e] = v;
+  }
+  if constexpr (GEOM == kGeomOTF) {
+    for (int e = tid; e < 2 * NV; e += NT) s_X[0][e] = vertex(e / NV, e % NV);
+  }
+  for (int e = tid; e < PL; e += NT) s_c[0][e] = T(0);
 
-  // ---- prologue: first layer's planes and carry init
-  for (int e = tid; e < S::slab; e += blockDim.x) s_y[e] = T(0);
-  load_planes(0, 0, ND);
+  // Per-thread vertex-derived geometry coefficients for the current layer.
+  T Js[3] = {0, 0, 0};                        // dX/ds at (t_a, u_b): constant in s
+  T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};   // dX/dt = Jt0 + s Jt1
+  T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};   // dX/du = Ju0 + s Ju1
 
   for (int64_t cx = 0; cx < ncx; ++cx) {
-    // Opaque zero: stops the compiler hoisting the 1D-table reads out of the
-    // x-march (they would pin ~2*(NQ^2 + NQ*ND) registers for the whole loop).
+    const int cur = static_cast<int>(cx & 1), nxt = cur ^ 1;
+    const bool last = (cx == ncx - 1);
+    __syncthreads();  // staged buffers of this layer complete
+
+    // ---- prefetch the next layer (planes 1..P of x-layer cx+1, vertex plane cx+2)
+    T pf_r[NPF], pf_p[NPF];
+    T pf_v[NPV];
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      pf_r[k] = T(0);
+      pf_p[k] = T(0);
+      const int e = tid + k * NT;
+      if (!last && e < P * PL) {
+        const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+        if (ly < ey && lz < ez) {
+          const int64_t id = lat.idx((cx + 1) * P + pl, y0 + ly, z0 + lz);
+          pf_r[k] = A.u[id];
+          if constexpr (MODE == kFusedCG) pf_p[k] = A.pold[id];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPV; ++k) {
+      pf_v[k] = T(0);
+      if constexpr (GEOM == kGeomOTF) {
+        const int e = tid + k * NT;
+        if (!last && e < NV) pf_v[k] = vertex(cx + 2, e);
+      }
+    }
+
+    // Opaque zero: keeps the 1D-table reads inside the layer (no hoisting).
     int toff = 0;
     asm volatile("" : "+s"(toff));
     const T* __restrict__ Dm = s_dphi + toff;  // dphi1[q][m]
     const T* __restrict__ Ph = s_phi + toff;   // phi0[q][i]
-    if constexpr (GEOM == kGeomOTF) {
-      // vertex planes x = cx, cx+1 of the tile
-      constexpr int nv = 2 * (TY + 1) * (TZ + 1) * 3;
-      for (int e = tid; e < nv; e += blockDim.x) {
-        const int d = e % 3, r = e / 3;
-        const int vz = r % (TZ + 1), vy = (r / (TZ + 1)) % (TY + 1), vx = r / ((TY + 1) * (TZ + 1));
-        const int64_t gy = static_cast<int64_t>(ty) * TY + vy, gz = static_cast<int64_t>(tz) * TZ + vz;
-        T val = T(0);
-        if (gy <= lat.n[1] && gz <= lat.n[2]) val = A.xv[3 * lat.vidx(cx + vx, gy, gz) + d];
-        s_X[vx][vy][vz][d] = val;
-      }
-    }
-    __syncthreads();
+    const T* __restrict__ su = s_u[cur];
+    const T* __restrict__ sX = s_X[cur];
 
-    // ------------------------------------------------ interpolate to qpts
     // per-thread LDS bases: every access below is base + compile-time offset
-    const T* __restrict__ ua = s_u + (yb + a) * DZ + zb;
+    const T* __restrict__ ua = su + (yb + a) * DZ + zb;
     T* __restrict__ w1ab = w1c + (a * NQ + b) * NQ;
     T* __restrict__ w2ab = w2c + (a * NQ + b) * NQ;
     T* __restrict__ w3ab = w3c + (a * NQ + b) * NQ;
@@ -244,11 +274,11 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
     const T* __restrict__ DmTa = Dm + a;       // dphi1[.][a]
     const T* __restrict__ DmTb = Dm + b;       // dphi1[.][b]
 
+    // ------------------------------------------------ interpolate to qpts
     T U[NQ];
     if constexpr (IDENT) {
 #pragma unroll
-      for (int i = 0; i < NQ; ++i)
-        U[i] = lane_on ? ua[i * DY * DZ + b] : T(0);
+      for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[i * PL + b] : T(0);
     } else {
       // S1: z-interp, thread (c, a=j<ND, b=qz): w1[a][b][i]
       if (lane_on && a < ND) {
@@ -256,7 +286,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
         for (int i = 0; i < ND; ++i) {
           T acc = 0;
 #pragma unroll
-          for (int k = 0; k < ND; ++k) acc += Ph[b * ND + k] * ua[i * DY * DZ + k];
+          for (int k = 0; k < ND; ++k) acc += Ph[b * ND + k] * ua[i * PL + k];
           w1ab[i] = acc;
         }
       }
@@ -282,14 +312,15 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
 
     // ------------------------------------------------ geometry coefficients
     if constexpr (GEOM == kGeomOTF) {
-      // bilinear coefficients of this column (cell (cy, cz), point (t_a, u_b))
       const T t = s_qw[a], u = s_qw[b];
+      const T* X0 = sX;        // plane cx
+      const T* X1 = sX + NV;   // plane cx+1
+      const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
+      const int v10 = v00 + (TZ + 1) * 3, v11 = v10 + 3;
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
-        const T X000 = s_X[0][cy][cz][d], X001 = s_X[0][cy][cz + 1][d];
-        const T X010 = s_X[0][cy + 1][cz][d], X011 = s_X[0][cy + 1][cz + 1][d];
-        const T X100 = s_X[1][cy][cz][d], X101 = s_X[1][cy][cz + 1][d];
-        const T X110 = s_X[1][cy + 1][cz][d], X111 = s_X[1][cy + 1][cz + 1][d];
+        const T X000 = X0[v00 + d], X001 = X0[v01 + d], X010 = X0[v10 + d], X011 = X0[v11 + d];
+        const T X100 = X1[v00 + d], X101 = X1[v01 + d], X110 = X1[v10 + d], X111 = X1[v11 + d];
         Js[d] = (1 - t) * ((1 - u) * (X100 - X000) + u * (X101 - X001)) +
                 t * ((1 - u) * (X110 - X010) + u * (X111 - X011));
         Jt0[d] = (1 - u) * (X010 - X000) + u * (X011 - X001);
@@ -314,7 +345,6 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
     T Fx[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      BDX_SCHED_FENCE();
       T gx = 0, gy = 0, gz = 0;
 #pragma unroll
       for (int m = 0; m < NQ; ++m) {
@@ -324,7 +354,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       }
       T fx, fy, fz;
       if constexpr (GEOM == kGeomOTF) {
-        const T s = tb.qpts[q];
+        const T s = s_qw[q];
         const T J00 = Js[0], J10 = Js[1], J20 = Js[2];
         const T J01 = Jt0[0] + s * Jt1[0], J11 = Jt0[1] + s * Jt1[1], J21 = Jt0[2] + s * Jt1[2];
         const T J02 = Ju0[0] + s * Ju1[0], J12 = Ju0[1] + s * Ju1[1], J22 = Ju0[2] + s * Ju1[2];
@@ -333,7 +363,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
         const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
         const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
         const T det = J00 * K00 + J01 * K10 + J02 * K20;
-        const T sc = kwyz * tb.wts[q] / det;
+        const T sc = kwyz * s_qw[NQ + q] / det;
         // h = K^T g, F = sc K h  (= kappa w det J^-1 J^-T g)
         const T h0 = K00 * gx + K10 * gy + K20 * gz;
         const T h1 = K01 * gx + K11 * gy + K21 * gz;
@@ -367,7 +397,6 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
     for (int i = 0; i < ND; ++i) sx[i] = 0;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      BDX_SCHED_FENCE();
       T acc = 0;
 #pragma unroll
       for (int m = 0; m < NQ; ++m) {
@@ -419,62 +448,77 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       }
     }
 
-    // ------------------------------------------------ scatter into the slab
+    // ------------------------------------------------ element vectors -> LDS
     const bool dof_lane = cell_on && a < ND && b < ND;
     if constexpr (MODE == kFusedCG) {
       if (dof_lane) {
 #pragma unroll
         for (int i = 0; i < ND; ++i)
-          pap += static_cast<double>(ua[i * DY * DZ + b]) * static_cast<double>(ye[i]);
+          pap += static_cast<double>(ua[i * PL + b]) * static_cast<double>(ye[i]);
       }
     }
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      if (dof_lane && ((cy & 1) * 2 + (cz & 1)) == ph) {
-#pragma unroll
-        for (int i = 0; i < ND; ++i) s_y[(yb + a) * DZ + zb + b + i * DY * DZ] += ye[i];
-      }
-      __syncthreads();
+    if constexpr (IDENT) {
+      __syncthreads();  // all reads of w2 (the gradient stage) done
     }
+    if (lane_on && a < ND && b < ND) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) w2ab[i] = dof_lane ? ye[i] : T(0);
+    }
+    __syncthreads();
 
-    // ------------------------------------------------ write out the layer
-    const bool last = (cx == ncx - 1);
-    const int npl = last ? ND : P;
-    {
-      const int n = npl * DY * DZ;
-      for (int e = tid; e < n; e += blockDim.x) {
-        const int pl = e / (DY * DZ);
-        const int rem = e % (DY * DZ);
-        const int ly = rem / DZ, lz = rem % DZ;
-        if (ly >= ey || lz >= ez) continue;
-        const int64_t gx = cx * P + pl, gy = y0 + ly, gz = z0 + lz;
-        const bool bc = gbc(gx, gy, gz);
-        const T v = bc ? T(0) : s_y[e];
-        const bool iy = ly < oy, iz = lz < oz;
-        if (iy && iz) {
-          if (!bc) A.y[lat.idx(gx, gy, gz)] = v;
-        } else if (!iy && iz) {
-          A.yb[(gx * (A.nty - 1) + ty) * Lz + gz] = v;
-        } else if (iy && !iz) {
-          A.zb[(gx * Ly + gy) * (A.ntz - 1) + tz] = v;
-        } else {
-          A.cb[(gx * (A.nty - 1) + ty) * (A.ntz - 1) + tz] = v;
-        }
+    // ------------------------------------------------ gather-sum, write out, stage next layer
+    for (int e = tid; e < ND * PL; e += NT) {
+      const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      if (ly >= ey || lz >= ez) continue;
+      const int cyh = (ly / P < TY - 1) ? ly / P : TY - 1;
+      const int cyl = (ly % P == 0 && ly > 0 && ly / P - 1 < cyh) ? ly / P - 1 : cyh;
+      const int czh = (lz / P < TZ - 1) ? lz / P : TZ - 1;
+      const int czl = (lz % P == 0 && lz > 0 && lz / P - 1 < czh) ? lz / P - 1 : czh;
+      T v = (pl == 0) ? s_c[cur][rem] : T(0);
+      for (int ccy = cyl; ccy <= cyh; ++ccy)
+        for (int ccz = czl; ccz <= czh; ++ccz)
+          v += s_w2[((ccy * TZ + ccz) * NQ + (ly - ccy * P)) * NQ2 + (lz - ccz * P) * NQ + pl];
+      if (pl == P && !last) {
+        s_c[nxt][rem] = v;
+        continue;
+      }
+      const int64_t gx = cx * P + pl, gy = y0 + ly, gz = z0 + lz;
+      const bool bc = lat.is_bc(gx, gy, gz);
+      if (bc) v = T(0);
+      const bool iy = ly < oy, iz = lz < oz;
+      if (iy && iz) {
+        if (!bc) A.y[lat.idx(gx, gy, gz)] = v;
+      } else if (!iy && iz) {
+        A.yb[(gx * (A.nty - 1) + ty) * Lz + gz] = v;
+      } else if (iy && !iz) {
+        A.zb[(gx * Ly + gy) * (A.ntz - 1) + tz] = v;
+      } else {
+        A.cb[(gx * (A.nty - 1) + ty) * (A.ntz - 1) + tz] = v;
       }
     }
     if (!last) {
-      __syncthreads();
-      // carry plane P -> plane 0, clear the others; shift the input slab
-      for (int e = tid; e < DY * DZ; e += blockDim.x) {
-        s_y[e] = s_y[P * DY * DZ + e];
-        s_u[e] = s_u[P * DY * DZ + e];
+      T* __restrict__ un = s_u[nxt];
+      for (int e = tid; e < PL; e += NT) un[e] = su[P * PL + e];
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) {
+        const int e = tid + k * NT;
+        if (e < P * PL) {
+          const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+          T v = T(0);
+          if (ly < ey && lz < ez) v = stage((cx + 1) * P + pl, ly, lz, pf_r[k], pf_p[k]);
+          un[PL + e] = v;
+        }
       }
-      for (int e = tid; e < P * DY * DZ; e += blockDim.x) s_y[DY * DZ + e] = T(0);
-      __syncthreads();
-      load_planes(cx + 1, 1, ND);
+      if constexpr (GEOM == kGeomOTF) {
+        for (int e = tid; e < NV; e += NT) s_X[nxt][e] = sX[NV + e];
+#pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][NV + e] = pf_v[k];
+        }
+      }
     }
   }
-  (void)Lx;
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
     if (tid == 0) A.partials[blockIdx.x] = t;
