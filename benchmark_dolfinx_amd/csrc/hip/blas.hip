@@ -116,15 +116,24 @@ __global__ void __launch_bounds__(kBlock)
 // Box table in device memory: per box {lo0,lo1,lo2, e0,e1,e2, offset} (int64).
 constexpr int kBoxFields = 7;
 
-template <typename T, int MODE>  // 0 pack, 1 unpack (assign), 2 unpack (add)
+// MODE 0 pack, 1 unpack (assign), 2 unpack (add).  `only` >= 0 restricts the
+// pass to one box: the owned lower-face boxes overlap on edges/corners (a dof
+// there receives partial sums from up to 7 neighbours), so the add-unpack runs
+// box by box -- race-free and in a fixed order.
+template <typename T, int MODE>
 __global__ void __launch_bounds__(kBlock)
     box_copy_kernel(T* __restrict__ vec, int64_t L1, int64_t ld,
                     const int64_t* __restrict__ boxes, int nboxes, int64_t total,
-                    T* __restrict__ buf) {
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < total;
+                    T* __restrict__ buf, int only = -1) {
+  int64_t t0 = 0, t1 = total;
+  if (only >= 0) {
+    t0 = boxes[only * kBoxFields + 6];
+    t1 = only + 1 < nboxes ? boxes[(only + 1) * kBoxFields + 6] : total;
+  }
+  for (int64_t t = t0 + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < t1;
        t += static_cast<int64_t>(gridDim.x) * kBlock) {
-    int b = 0;
-    while (b + 1 < nboxes && boxes[(b + 1) * kBoxFields + 6] <= t) ++b;
+    int b = only >= 0 ? only : 0;
+    while (only < 0 && b + 1 < nboxes && boxes[(b + 1) * kBoxFields + 6] <= t) ++b;
     const int64_t* bx = boxes + b * kBoxFields;
     const int64_t o = t - bx[6];
     const int64_t e1 = bx[4], e2 = bx[5];
@@ -207,9 +216,10 @@ int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
     else if (mode == 1)                                                       \
       box_copy_kernel<T, 1><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
                                                   total, buf);                \
-    else                                                                      \
-      box_copy_kernel<T, 2><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
-                                                  total, buf);                \
+    else /* add: boxes may overlap (edges/corners), one launch per box */     \
+      for (int b = 0; b < nboxes; ++b)                                        \
+        box_copy_kernel<T, 2><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
+                                                    total, buf, b);           \
     return static_cast<int>(hipGetLastError());                               \
   }
 

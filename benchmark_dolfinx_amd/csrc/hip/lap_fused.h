@@ -35,11 +35,20 @@ enum { kFusedAction = 0, kFusedCG = 1 };
 // hoisting every LDS read of a fully unrolled stage to its top (which costs
 // hundreds of registers and occupancy).
 // Pin values computed in an unrolled iteration before the next iteration's
-// LDS reads (the memory clobber keeps those reads below; the register
-// operands keep this iteration's FMAs above).  Without it the scheduler
-// issues every read of a stage first and spills the results.
-#define BDX_PIN1(x) asm volatile("" : "+v"(x)::"memory")
-#define BDX_PIN3(x, y, z) asm volatile("" : "+v"(x), "+v"(y), "+v"(z)::"memory")
+// LDS reads (the register operands keep this iteration's FMAs above the
+// fence; the scheduling barrier keeps the next reads below it).  Without it
+// the scheduler issues every read of a stage first and spills the results.
+// No memory clobber: the per-thread table rows stay CSE'd in registers.
+#define BDX_PIN1(x)                    \
+  do {                                 \
+    asm volatile("" : "+v"(x));        \
+    __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+#define BDX_PIN3(x, y, z)                              \
+  do {                                                 \
+    asm volatile("" : "+v"(x), "+v"(y), "+v"(z));      \
+    __builtin_amdgcn_sched_barrier(0);                 \
+  } while (0)
 
 #ifndef BDX_NO_SCHED_FENCE
 #define BDX_SCHED_FENCE()               \
@@ -63,6 +72,7 @@ struct FusedShape {
   static constexpr int threads = ((lanes + 63) / 64) * 64;
   static constexpr int DY = TY * P + 1;
   static constexpr int DZ = TZ * P + 1;
+  static constexpr int DZP = DZ | 1;  // odd LDS row pitch (bank spread)
   static constexpr int slab = ND * DY * DZ;   // one layer's dof slab
   static constexpr int work = cells * NQ * NQ * NQ;
 };
@@ -102,6 +112,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
     lap_fused_kernel(FusedArgs<T> A, OpTables<T> tb) {
   using S = FusedShape<ND, NQ, TY, TZ>;
   constexpr int P = S::P, DY = S::DY, DZ = S::DZ, PL = DY * DZ;
+  constexpr int DZP = S::DZP, PLP = DY * DZP;  // padded LDS pitches of the input slab
   constexpr int NQ2 = NQ * NQ;
   constexpr bool IDENT = (ND == NQ);
   constexpr int NT = S::threads;
@@ -112,7 +123,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
   __shared__ T s_phi[NQ * ND];        // phi0[q][i]
   __shared__ T s_dphi[NQ * NQ];       // dphi1[q][j]
   __shared__ T s_qw[2 * NQ];          // quadrature points, weights
-  __shared__ T s_u[2][ND * PL];       // input slab [pl][ly][lz] (BC dofs zeroed), double-buffered
+  __shared__ T s_u[2][ND * PLP];      // input slab [pl][ly][lz] (BC dofs zeroed), double-buffered
   __shared__ T s_c[2][PL];            // x-carried output plane, ping-pong
   __shared__ T s_w1[S::work];         // [c][a][b][x] scratch
   __shared__ T s_w2[S::work];
@@ -208,7 +219,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       const int64_t id = lat.idx(pl, y0 + ly, z0 + lz);
       v = stage(pl, ly, lz, A.u[id], MODE == kFusedCG ? A.pold[id] : T(0));
     }
-    s_u[0][e] = v;
+    s_u[0][pl * PLP + ly * DZP + lz] = v;
   }
   if constexpr (GEOM == kGeomOTF) {
     for (int e = tid; e < 2 * NV; e += NT) s_X[0][e] = vertex(e / NV, e % NV);
@@ -260,7 +271,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
     const T* __restrict__ sX = s_X[cur];
 
     // per-thread LDS bases: every access below is base + compile-time offset
-    const T* __restrict__ ua = su + (yb + a) * DZ + zb;
+    const T* __restrict__ ua = su + (yb + a) * DZP + zb;
     T* __restrict__ w1ab = w1c + (a * NQ + b) * NQ;
     T* __restrict__ w2ab = w2c + (a * NQ + b) * NQ;
     T* __restrict__ w3ab = w3c + (a * NQ + b) * NQ;
@@ -278,7 +289,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
     T U[NQ];
     if constexpr (IDENT) {
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[i * PL + b] : T(0);
+      for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[i * PLP + b] : T(0);
     } else {
       // S1: z-interp, thread (c, a=j<ND, b=qz): w1[a][b][i]
       if (lane_on && a < ND) {
@@ -286,7 +297,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
         for (int i = 0; i < ND; ++i) {
           T acc = 0;
 #pragma unroll
-          for (int k = 0; k < ND; ++k) acc += Ph[b * ND + k] * ua[i * PL + k];
+          for (int k = 0; k < ND; ++k) acc += Ph[b * ND + k] * ua[i * PLP + k];
           w1ab[i] = acc;
         }
       }
@@ -454,7 +465,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       if (dof_lane) {
 #pragma unroll
         for (int i = 0; i < ND; ++i)
-          pap += static_cast<double>(ua[i * PL + b]) * static_cast<double>(ye[i]);
+          pap += static_cast<double>(ua[i * PLP + b]) * static_cast<double>(ye[i]);
       }
     }
     if constexpr (IDENT) {
@@ -498,7 +509,10 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
     }
     if (!last) {
       T* __restrict__ un = s_u[nxt];
-      for (int e = tid; e < PL; e += NT) un[e] = su[P * PL + e];
+      for (int e = tid; e < PL; e += NT) {
+        const int o = (e / DZ) * DZP + e % DZ;
+        un[o] = su[P * PLP + o];
+      }
 #pragma unroll
       for (int k = 0; k < NPF; ++k) {
         const int e = tid + k * NT;
@@ -506,7 +520,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
           const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
           T v = T(0);
           if (ly < ey && lz < ez) v = stage((cx + 1) * P + pl, ly, lz, pf_r[k], pf_p[k]);
-          un[PL + e] = v;
+          un[pl * PLP + ly * DZP + lz] = v;
         }
       }
       if constexpr (GEOM == kGeomOTF) {
