@@ -60,11 +60,29 @@ enum { kFusedAction = 0, kFusedCG = 1 };
 #define BDX_SCHED_FENCE()
 #endif
 
-#ifndef BDX_FUSED_WAVES
-#define BDX_FUSED_WAVES 1
+// Minimum waves per SIMD requested from the register allocator (the LDS
+// footprint allows 3 workgroups/CU up to nq=6 and 2 beyond).  Override with
+// -DBDX_FUSED_WAVES=n for experiments.
+template <int NQ>
+struct FusedWaves {
+#ifdef BDX_FUSED_WAVES
+  static constexpr int value = BDX_FUSED_WAVES;
+#else
+  static constexpr int value = NQ <= 6 ? 3 : 2;
 #endif
+};
 
-template <int ND, int NQ, int TY, int TZ>
+template <typename T> struct VecOf;
+template <> struct VecOf<double> {
+  typedef double __attribute__((ext_vector_type(2))) type;
+  static constexpr int W = 2;
+};
+template <> struct VecOf<float> {
+  typedef float __attribute__((ext_vector_type(4))) type;
+  static constexpr int W = 4;
+};
+
+template <typename T, int ND, int NQ, int TY, int TZ>
 struct FusedShape {
   static constexpr int P = ND - 1;
   static constexpr int cells = TY * TZ;
@@ -72,10 +90,45 @@ struct FusedShape {
   static constexpr int threads = ((lanes + 63) / 64) * 64;
   static constexpr int DY = TY * P + 1;
   static constexpr int DZ = TZ * P + 1;
-  static constexpr int DZP = DZ | 1;  // odd LDS row pitch (bank spread)
-  static constexpr int slab = ND * DY * DZ;   // one layer's dof slab
-  static constexpr int work = cells * NQ * NQ * NQ;
+  static constexpr int DZP = DZ | 1;  // odd LDS row pitch of the input slab (bank spread)
+  static constexpr int VW = VecOf<T>::W;
+  static constexpr int XP = (NQ + VW - 1) / VW * VW;  // 16-byte aligned row pitch (x axis)
+  static constexpr int NP = (ND + VW - 1) / VW * VW;
+  static constexpr int work = cells * NQ * NQ * XP;   // [c][a][b][x] scratch
+  // packed 1D tables (host: bdx_fused_tables): rows padded for vector reads
+  static constexpr int OFF_DR = 0;                  // Dr[q][m] = dphi1[q][m]
+  static constexpr int OFF_DC = NQ * XP;            // Dc[m][q] = dphi1[q][m]
+  static constexpr int OFF_PR = 2 * NQ * XP;        // Pr[q][i] = phi0[q][i]   (pitch NP)
+  static constexpr int OFF_PC = 2 * NQ * XP + NQ * NP;  // Pc[i][q] = phi0[q][i]
+  static constexpr int TAB = OFF_PC + ND * XP;
 };
+
+// 16-byte vector row load / store (p 16-byte aligned, row padded to the
+// vector width; the tail of the last vector reads/writes padding).
+template <int N, typename T>
+__device__ __forceinline__ void ldrow(const T* __restrict__ p, T (&o)[N]) {
+  using V = typename VecOf<T>::type;
+  constexpr int W = VecOf<T>::W;
+#pragma unroll
+  for (int k = 0; k < N; k += W) {
+    const V v = *reinterpret_cast<const V*>(p + k);
+#pragma unroll
+    for (int e = 0; e < W; ++e)
+      if (k + e < N) o[k + e] = v[e];
+  }
+}
+template <int N, typename T>
+__device__ __forceinline__ void strow(T* __restrict__ p, const T (&x)[N]) {
+  using V = typename VecOf<T>::type;
+  constexpr int W = VecOf<T>::W;
+#pragma unroll
+  for (int k = 0; k < N; k += W) {
+    V v;
+#pragma unroll
+    for (int e = 0; e < W; ++e) v[e] = (k + e < N) ? x[k + e] : T(0);
+    *reinterpret_cast<V*>(p + k) = v;
+  }
+}
 
 // Tile selection per (ND, NQ): as many whole cells as fit in 256 lanes.
 template <int NQ> struct TileFor;
@@ -87,6 +140,16 @@ template <> struct TileFor<6> { static constexpr int TY = 1, TZ = 7; };
 template <> struct TileFor<7> { static constexpr int TY = 1, TZ = 5; };
 template <> struct TileFor<8> { static constexpr int TY = 2, TZ = 2; };
 template <> struct TileFor<9> { static constexpr int TY = 1, TZ = 3; };
+
+// Packed 1D tables + quadrature, passed by value in the kernarg segment
+// (constant address space: wave-uniform reads become scalar loads).
+constexpr int kFusedTabMax = 2 * 9 * 12 + 9 * 8 + 8 * 12;  // TAB for nd=8, nq=9 (f32 pitch)
+template <typename T>
+struct FusedTables {
+  T tab[kFusedTabMax];
+  T qpts[kMaxNq];
+  T wts[kMaxNq];
+};
 
 template <typename T>
 struct FusedArgs {
@@ -108,9 +171,9 @@ struct FusedArgs {
 };
 
 template <typename T, int ND, int NQ, int TY, int TZ, int GEOM, int MODE>
-__global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUSED_WAVES)
-    lap_fused_kernel(FusedArgs<T> A, OpTables<T> tb) {
-  using S = FusedShape<ND, NQ, TY, TZ>;
+__global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
+    lap_fused_kernel(FusedArgs<T> A, FusedTables<T> tb) {
+  using S = FusedShape<T, ND, NQ, TY, TZ>;
   constexpr int P = S::P, DY = S::DY, DZ = S::DZ, PL = DY * DZ;
   constexpr int DZP = S::DZP, PLP = DY * DZP;  // padded LDS pitches of the input slab
   constexpr int NQ2 = NQ * NQ;
@@ -120,21 +183,21 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
   constexpr int NV = (TY + 1) * (TZ + 1) * 3;          // vertex values per plane
   constexpr int NPV = (NV + NT - 1) / NT;
 
-  __shared__ T s_phi[NQ * ND];        // phi0[q][i]
-  __shared__ T s_dphi[NQ * NQ];       // dphi1[q][j]
+  constexpr int XP = S::XP, NP = S::NP;
+  __shared__ __attribute__((aligned(16))) T s_tab[S::TAB];  // per-thread table rows
   __shared__ T s_qw[2 * NQ];          // quadrature points, weights
   __shared__ T s_u[2][ND * PLP];      // input slab [pl][ly][lz] (BC dofs zeroed), double-buffered
   __shared__ T s_c[2][PL];            // x-carried output plane, ping-pong
-  __shared__ T s_w1[S::work];         // [c][a][b][x] scratch
-  __shared__ T s_w2[S::work];
-  __shared__ T s_w3[S::work];
+  __shared__ __attribute__((aligned(16))) T s_w1[S::work];  // [c][a][b][x] scratch, pitch XP
+  __shared__ __attribute__((aligned(16))) T s_w2[S::work];
+  __shared__ __attribute__((aligned(16))) T s_w3[S::work];
   __shared__ T s_X[2][2 * NV];        // vertex planes (cx, cx+1) of the tile, double-buffered
   __shared__ double s_red[16];
 
   const BdxLattice& lat = A.lat;
   const int tid = threadIdx.x;
-  for (int i = tid; i < NQ * ND; i += NT) s_phi[i] = tb.phi0[i];
-  for (int i = tid; i < NQ * NQ; i += NT) s_dphi[i] = tb.dphi1[i];
+  static_assert(S::TAB <= kFusedTabMax, "table too large");
+  for (int i = tid; i < S::TAB; i += NT) s_tab[i] = tb.tab[i];
   if (tid < NQ) {
     s_qw[tid] = tb.qpts[tid];
     s_qw[NQ + tid] = tb.wts[tid];
@@ -165,9 +228,9 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
   const bool cell_on = lane_on && (static_cast<int64_t>(ty) * TY + cy < lat.n[1]) &&
                        (static_cast<int64_t>(tz) * TZ + cz < lat.n[2]);
   const int yb = cy * P, zb = cz * P;
-  T* w1c = s_w1 + c * NQ * NQ2;
-  T* w2c = s_w2 + c * NQ * NQ2;
-  T* w3c = s_w3 + c * NQ * NQ2;
+  T* w1c = s_w1 + c * NQ2 * XP;
+  T* w2c = s_w2 + c * NQ2 * XP;
+  T* w3c = s_w3 + c * NQ2 * XP;
 
   T beta = T(0);
   if constexpr (MODE == kFusedCG) {
@@ -262,28 +325,24 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       }
     }
 
-    // Opaque zero: keeps the 1D-table reads inside the layer (no hoisting).
+    // Opaque zero: keeps the uniform table reads (scalar loads into SGPRs)
+    // inside the layer instead of pinning them for the whole x-march.
     int toff = 0;
     asm volatile("" : "+s"(toff));
-    const T* __restrict__ Dm = s_dphi + toff;  // dphi1[q][m]
-    const T* __restrict__ Ph = s_phi + toff;   // phi0[q][i]
+    const T* __restrict__ gt = tb.tab + toff;  // wave-uniform rows -> SMEM (kernarg)
     const T* __restrict__ su = s_u[cur];
     const T* __restrict__ sX = s_X[cur];
 
-    // per-thread LDS bases: every access below is base + compile-time offset
+    // per-thread LDS bases (rows of pitch XP, 16-byte aligned)
     const T* __restrict__ ua = su + (yb + a) * DZP + zb;
-    T* __restrict__ w1ab = w1c + (a * NQ + b) * NQ;
-    T* __restrict__ w2ab = w2c + (a * NQ + b) * NQ;
-    T* __restrict__ w3ab = w3c + (a * NQ + b) * NQ;
-    const T* __restrict__ w1b = w1c + b * NQ;
-    const T* __restrict__ w2b = w2c + b * NQ;
-    const T* __restrict__ w1a = w1c + a * NQ2;
-    const T* __restrict__ w2a = w2c + a * NQ2;
-    const T* __restrict__ w3a = w3c + a * NQ2;
-    const T* __restrict__ Dma = Dm + a * NQ;   // dphi1[a][.]
-    const T* __restrict__ Dmb = Dm + b * NQ;   // dphi1[b][.]
-    const T* __restrict__ DmTa = Dm + a;       // dphi1[.][a]
-    const T* __restrict__ DmTb = Dm + b;       // dphi1[.][b]
+    T* __restrict__ w1ab = w1c + (a * NQ + b) * XP;
+    T* __restrict__ w2ab = w2c + (a * NQ + b) * XP;
+    T* __restrict__ w3ab = w3c + (a * NQ + b) * XP;
+    const T* __restrict__ w1b = w1c + b * XP;        // + m * NQ * XP : [c][m][b][.]
+    const T* __restrict__ w2b = w2c + b * XP;
+    const T* __restrict__ w1a = w1c + a * NQ * XP;   // + m * XP      : [c][a][m][.]
+    const T* __restrict__ w2a = w2c + a * NQ * XP;
+    const T* __restrict__ w3a = w3c + a * NQ * XP;
 
     // ------------------------------------------------ interpolate to qpts
     T U[NQ];
@@ -291,33 +350,66 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
 #pragma unroll
       for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[i * PLP + b] : T(0);
     } else {
-      // S1: z-interp, thread (c, a=j<ND, b=qz): w1[a][b][i]
+      // S1: z-interp, thread (c, a=j<ND, b=qz): w1[c][j][qz][i]
       if (lane_on && a < ND) {
+        const T* __restrict__ ph = s_tab + S::OFF_PR + b * NP;
+        T o[ND];
 #pragma unroll
-        for (int i = 0; i < ND; ++i) {
-          T acc = 0;
+        for (int i = 0; i < ND; ++i) o[i] = 0;
+#pragma unroll 1
+        for (int k = 0; k < ND; ++k) {
+          const T c = ph[k];
 #pragma unroll
-          for (int k = 0; k < ND; ++k) acc += Ph[b * ND + k] * ua[i * PLP + k];
-          w1ab[i] = acc;
+          for (int i = 0; i < ND; ++i) o[i] += c * ua[i * PLP + k];
         }
+        strow<ND>(w1ab, o);
       }
       __syncthreads();
-      // S2: y-interp, thread (c, a=qy, b=qz)
+      // S2: y-interp, thread (c, a=qy, b=qz): t2[i] = sum_j phi0[a][j] w1[c][j][b][i]
+      const T* __restrict__ pa = s_tab + S::OFF_PR + a * NP;
       T t2[ND];
 #pragma unroll
-      for (int i = 0; i < ND; ++i) {
-        T acc = 0;
+      for (int i = 0; i < ND; ++i) t2[i] = 0;
+#pragma unroll 1
+      for (int j = 0; j < ND; ++j) {
+        T row[ND];
+        ldrow<ND>(w1b + j * NQ * XP, row);
+        const T c = pa[j];
 #pragma unroll
-        for (int j = 0; j < ND; ++j) acc += Ph[a * ND + j] * w1b[j * NQ2 + i];
-        t2[i] = lane_on ? acc : T(0);
+        for (int i = 0; i < ND; ++i) t2[i] += c * row[i];
       }
-      // S3: x-interp in registers
+      // S3: x-interp in registers, uniform rows of phi0^T
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        T acc = 0;
+      for (int q = 0; q < NQ; ++q) U[q] = 0;
 #pragma unroll
-        for (int i = 0; i < ND; ++i) acc += Ph[q * ND + i] * t2[i];
-        U[q] = acc;
+      for (int i = 0; i < ND; ++i) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) U[q] += gt[S::OFF_PC + i * XP + q] * t2[i];
+      }
+    }
+
+    // ------------------------------------------------ reference gradient (m-outer)
+    if (lane_on) strow<NQ>(w2ab, U);
+    __syncthreads();
+    T gx[NQ], gy[NQ], gz[NQ];
+    {
+      const T* __restrict__ dra = s_tab + S::OFF_DR + a * XP;   // dphi1[a][.]
+      const T* __restrict__ drb = s_tab + S::OFF_DR + b * XP;   // dphi1[b][.]
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) gx[q] = gy[q] = gz[q] = 0;
+#pragma unroll 1
+      for (int m = 0; m < NQ; ++m) {
+        T ry[NQ], rz[NQ];
+        ldrow<NQ>(w2b + m * NQ * XP, ry);   // U[c][m][b][.]
+        ldrow<NQ>(w2a + m * XP, rz);        // U[c][a][m][.]
+        const T um = w2ab[m], cy_ = dra[m], cz_ = drb[m];
+        const T* __restrict__ dc = gt + S::OFF_DC + m * XP;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          gx[q] += dc[q] * um;
+          gy[q] += cy_ * ry[q];
+          gz[q] += cz_ * rz[q];
+        }
       }
     }
 
@@ -347,22 +439,13 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
                static_cast<int64_t>(tz) * TZ + cz) * 6 * (NQ * NQ2) + a * NQ + b;
     }
 
-    // ------------------------------------------------ gradient -> F (streamed over x)
-    if (lane_on) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) w2ab[q] = U[q];
-    }
-    __syncthreads();
+    // ------------------------------------------------ F = kappa G grad
     T Fx[NQ];
+    using V = typename VecOf<T>::type;
+    constexpr int VW = VecOf<T>::W;
+    V vy, vz;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      T gx = 0, gy = 0, gz = 0;
-#pragma unroll
-      for (int m = 0; m < NQ; ++m) {
-        gx += Dm[q * NQ + m] * U[m];
-        gy += Dma[m] * w2b[m * NQ2 + q];
-        gz += Dmb[m] * w2a[m * NQ + q];
-      }
       T fx, fy, fz;
       if constexpr (GEOM == kGeomOTF) {
         const T s = s_qw[q];
@@ -376,9 +459,9 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
         const T det = J00 * K00 + J01 * K10 + J02 * K20;
         const T sc = kwyz * s_qw[NQ + q] / det;
         // h = K^T g, F = sc K h  (= kappa w det J^-1 J^-T g)
-        const T h0 = K00 * gx + K10 * gy + K20 * gz;
-        const T h1 = K01 * gx + K11 * gy + K21 * gz;
-        const T h2 = K02 * gx + K12 * gy + K22 * gz;
+        const T h0 = K00 * gx[q] + K10 * gy[q] + K20 * gz[q];
+        const T h1 = K01 * gx[q] + K11 * gy[q] + K21 * gz[q];
+        const T h2 = K02 * gx[q] + K12 * gy[q] + K22 * gz[q];
         fx = sc * (K00 * h0 + K01 * h1 + K02 * h2);
         fy = sc * (K10 * h0 + K11 * h1 + K12 * h2);
         fz = sc * (K20 * h0 + K21 * h1 + K22 * h2);
@@ -389,38 +472,60 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
 #pragma unroll
           for (int k = 0; k < 6; ++k) Gd[k] = __builtin_nontemporal_load(g + k * NQ * NQ2);
         }
-        fx = A.kappa * (Gd[0] * gx + Gd[1] * gy + Gd[2] * gz);
-        fy = A.kappa * (Gd[1] * gx + Gd[3] * gy + Gd[4] * gz);
-        fz = A.kappa * (Gd[2] * gx + Gd[4] * gy + Gd[5] * gz);
+        fx = A.kappa * (Gd[0] * gx[q] + Gd[1] * gy[q] + Gd[2] * gz[q]);
+        fy = A.kappa * (Gd[1] * gx[q] + Gd[3] * gy[q] + Gd[4] * gz[q]);
+        fz = A.kappa * (Gd[2] * gx[q] + Gd[4] * gy[q] + Gd[5] * gz[q]);
       }
       BDX_PIN3(fx, fy, fz);
       Fx[q] = fx;
-      if (lane_on) {
-        w1ab[q] = fy;
-        w3ab[q] = fz;
+      vy[q % VW] = fy;
+      vz[q % VW] = fz;
+      if (q % VW == VW - 1 || q == NQ - 1) {
+        if (q % VW != VW - 1) {
+#pragma unroll
+          for (int e = q % VW + 1; e < VW; ++e) vy[e] = vz[e] = T(0);
+        }
+        if (lane_on) {
+          *reinterpret_cast<V*>(w1ab + (q / VW) * VW) = vy;
+          *reinterpret_cast<V*>(w3ab + (q / VW) * VW) = vz;
+        }
       }
     }
     __syncthreads();
 
-    // ------------------------------------------------ transposed gradient (+ x interp^T)
-    T sx[ND];
+    // ------------------------------------------------ transposed gradient (m-outer)
+    T r[NQ];
+    {
+      // Fx goes to this thread's own w2 row (all U reads finished at the
+      // barrier above; only this lane reads it back: no further barrier).
+      if (lane_on) strow<NQ>(w2ab, Fx);
+      const T* __restrict__ dca = s_tab + S::OFF_DC + a * XP;   // dphi1[.][a]
+      const T* __restrict__ dcb = s_tab + S::OFF_DC + b * XP;   // dphi1[.][b]
 #pragma unroll
-    for (int i = 0; i < ND; ++i) sx[i] = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      T acc = 0;
-#pragma unroll
+      for (int q = 0; q < NQ; ++q) r[q] = 0;
+#pragma unroll 1
       for (int m = 0; m < NQ; ++m) {
-        acc += Dm[m * NQ + q] * Fx[m];
-        acc += DmTa[m * NQ] * w1b[m * NQ2 + q];
-        acc += DmTb[m * NQ] * w3a[m * NQ + q];
-      }
-      BDX_PIN1(acc);
-      if constexpr (IDENT) {
-        sx[q] = acc;
-      } else {
+        T r1[NQ], r3[NQ];
+        ldrow<NQ>(w1b + m * NQ * XP, r1);   // Fy[c][m][b][.]
+        ldrow<NQ>(w3a + m * XP, r3);        // Fz[c][a][m][.]
+        const T fm = w2ab[m], ca = dca[m], cb = dcb[m];
+        const T* __restrict__ dr = gt + S::OFF_DR + m * XP;
 #pragma unroll
-        for (int i = 0; i < ND; ++i) sx[i] += Ph[q * ND + i] * acc;
+        for (int q = 0; q < NQ; ++q) r[q] += dr[q] * fm + ca * r1[q] + cb * r3[q];
+      }
+    }
+    // S7: x interp^T in registers, uniform rows of phi0^T
+    T sx[ND];
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) sx[i] = r[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        T acc = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc += gt[S::OFF_PC + i * XP + q] * r[q];
+        sx[i] = acc;
       }
     }
 
@@ -431,31 +536,38 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       for (int i = 0; i < ND; ++i) ye[i] = sx[i];
     } else {
       __syncthreads();  // reads of w1/w3 done
-      if (lane_on) {
-#pragma unroll
-        for (int i = 0; i < ND; ++i) w2ab[i] = sx[i];
-      }
+      if (lane_on) strow<ND>(w2ab, sx);
       __syncthreads();
-      // S8: y, thread (c, a=j<ND, b=qz)
+      // S8: y, thread (c, a=j<ND, b=qz): w1[c][j][qz][i] = sum_q phi0[q][j] w2[c][q][qz][i]
       if (lane_on && a < ND) {
+        const T* __restrict__ pca = s_tab + S::OFF_PC + a * XP;
+        T o[ND];
 #pragma unroll
-        for (int i = 0; i < ND; ++i) {
-          T acc = 0;
+        for (int i = 0; i < ND; ++i) o[i] = 0;
+#pragma unroll 1
+        for (int q = 0; q < NQ; ++q) {
+          T row[ND];
+          ldrow<ND>(w2b + q * NQ * XP, row);
+          const T c = pca[q];
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) acc += Ph[q * ND + a] * w2b[q * NQ2 + i];
-          w1ab[i] = acc;
+          for (int i = 0; i < ND; ++i) o[i] += c * row[i];
         }
+        strow<ND>(w1ab, o);
       }
       __syncthreads();
-      // S9: z, thread (c, a=j<ND, b=k<ND)
+      // S9: z, thread (c, a=j<ND, b=k<ND): ye[i] = sum_q phi0[q][k] w1[c][j][q][i]
 #pragma unroll
-      for (int i = 0; i < ND; ++i) {
-        T acc = 0;
-        if (a < ND && b < ND) {
+      for (int i = 0; i < ND; ++i) ye[i] = 0;
+      if (a < ND && b < ND) {
+        const T* __restrict__ pcb = s_tab + S::OFF_PC + b * XP;
+#pragma unroll 1
+        for (int q = 0; q < NQ; ++q) {
+          T row[ND];
+          ldrow<ND>(w1a + q * XP, row);
+          const T c = pcb[q];
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) acc += Ph[q * ND + b] * w1a[q * NQ + i];
+          for (int i = 0; i < ND; ++i) ye[i] += c * row[i];
         }
-        ye[i] = acc;
       }
     }
 
@@ -472,8 +584,11 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       __syncthreads();  // all reads of w2 (the gradient stage) done
     }
     if (lane_on && a < ND && b < ND) {
+      if (!dof_lane) {
 #pragma unroll
-      for (int i = 0; i < ND; ++i) w2ab[i] = dof_lane ? ye[i] : T(0);
+        for (int i = 0; i < ND; ++i) ye[i] = T(0);
+      }
+      strow<ND>(w2ab, ye);
     }
     __syncthreads();
 
@@ -488,7 +603,7 @@ __global__ void __launch_bounds__((FusedShape<ND, NQ, TY, TZ>::threads), BDX_FUS
       T v = (pl == 0) ? s_c[cur][rem] : T(0);
       for (int ccy = cyl; ccy <= cyh; ++ccy)
         for (int ccz = czl; ccz <= czh; ++ccz)
-          v += s_w2[((ccy * TZ + ccz) * NQ + (ly - ccy * P)) * NQ2 + (lz - ccz * P) * NQ + pl];
+          v += s_w2[(((ccy * TZ + ccz) * NQ + (ly - ccy * P)) * NQ + (lz - ccz * P)) * XP + pl];
       if (pl == P && !last) {
         s_c[nxt][rem] = v;
         continue;

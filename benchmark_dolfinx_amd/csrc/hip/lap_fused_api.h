@@ -5,9 +5,9 @@
 #include "lap_fused.h"
 
 template <typename T, int ND, int NQ, int GEOM, int MODE>
-int launch_fused(const FusedArgs<T>& a, const OpTables<T>& tb, hipStream_t st) {
+int launch_fused(const FusedArgs<T>& a, const FusedTables<T>& tb, hipStream_t st) {
   using TF = TileFor<NQ>;
-  using S = FusedShape<ND, NQ, TF::TY, TF::TZ>;
+  using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
   const int nblk = a.nty * a.ntz;
   if (nblk <= 0) return 0;
   lap_fused_kernel<T, ND, NQ, TF::TY, TF::TZ, GEOM, MODE>
@@ -16,7 +16,7 @@ int launch_fused(const FusedArgs<T>& a, const OpTables<T>& tb, hipStream_t st) {
 }
 
 template <typename T, int ND, int NQ>
-int launch_fused_any(int geom, int mode, const FusedArgs<T>& a, const OpTables<T>& tb,
+int launch_fused_any(int geom, int mode, const FusedArgs<T>& a, const FusedTables<T>& tb,
                      hipStream_t st) {
   if (geom == kGeomOTF) {
     return mode == kFusedCG ? launch_fused<T, ND, NQ, kGeomOTF, kFusedCG>(a, tb, st)
@@ -32,6 +32,7 @@ int launch_fused_any(int geom, int mode, const FusedArgs<T>& a, const OpTables<T
       int geom, int mode, const int64_t* latd, int nq, const double* phi0,        \
       const double* dphi1, const double* wts, const double* qpts, const T* u,     \
       const T* pold, T* pnew, T* y, T* yb, T* zb, T* cb, const T* G, const T* xv, \
+      const T* tabs /* host, kFusedTabMax values */,                              \
       double kappa, const double* scal, double* partials, int beta_num,           \
       int beta_den, int nty, int ntz, hipStream_t st) {                            \
     FusedArgs<T> a;                                                               \
@@ -52,8 +53,16 @@ int launch_fused_any(int geom, int mode, const FusedArgs<T>& a, const OpTables<T
     a.nty = nty;                                                                  \
     a.ntz = ntz;                                                                  \
     a.kappa = static_cast<T>(kappa);                                              \
-    const OpTables<T> tb = make_op_tables<T>(PP + 1, nq, phi0, dphi1, wts, qpts,  \
-                                             nq == PP + 1);                       \
+    FusedTables<T> tb;                                                            \
+    for (int i = 0; i < kFusedTabMax; ++i) tb.tab[i] = T(0);                      \
+    if (!tabs) return static_cast<int>(hipErrorInvalidValue);                     \
+    for (int i = 0; i < kFusedTabMax; ++i) tb.tab[i] = tabs[i];                   \
+    for (int q = 0; q < kMaxNq; ++q) {                                            \
+      tb.qpts[q] = q < nq ? static_cast<T>(qpts[q]) : T(0);                       \
+      tb.wts[q] = q < nq ? static_cast<T>(wts[q]) : T(0);                         \
+    }                                                                             \
+    (void)phi0;                                                                   \
+    (void)dphi1;                                                                  \
     if (nq == PP + 1) return launch_fused_any<T, PP + 1, PP + 1>(geom, mode, a, tb, st); \
     if (nq == PP + 2) return launch_fused_any<T, PP + 1, PP + 2>(geom, mode, a, tb, st); \
     return static_cast<int>(hipErrorInvalidValue);                                \

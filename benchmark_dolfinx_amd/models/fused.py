@@ -18,6 +18,7 @@ from __future__ import annotations
 import ctypes
 import math
 
+import numpy as np
 import torch
 
 from ..ops import native
@@ -64,6 +65,14 @@ class FusedLaplacianGPU:
             with timed("~setup geometry"):
                 self.G = torch.empty(lat.ncells_local * 6 * t.nq ** 3, dtype=dt, device=dev)
                 pb.kernels.geometry(pb.xv, self.G)
+        # packed 1D tables (uniform rows are read through scalar loads)
+        ftab = getattr(self.lib, f"bdx_fused_tables_{pb.suf}")
+        ntab = ftab(t.nd, t.nq, ptr(t.phi0), ptr(t.dphi1), None)
+        if ntab <= 0:
+            raise RuntimeError(f"no fused tables for nd={t.nd} nq={t.nq}")
+        host = np.zeros(ntab, dtype=np.float64 if pb.dtype == torch.float64 else np.float32)
+        ftab(t.nd, t.nq, ptr(t.phi0), ptr(t.dphi1), ptr(host))
+        self.tabs = host  # host memory: copied into the kernel arguments
         self._apply = getattr(self.lib, f"bdx_fused_apply_{pb.suf}_p{P}")
         self._final = getattr(self.lib, f"bdx_fused_finalize_{pb.suf}")
         self.geom_code = 1 if geometry == "otf" else 0
@@ -76,7 +85,7 @@ class FusedLaplacianGPU:
         _check(self._apply(self.geom_code, mode, ptr(pb.latd), t.nq, ptr(t.phi0), ptr(t.dphi1),
                            ptr(t.wts), ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(y),
                            ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(self.G), ptr(pb.xv),
-                           pb.kappa, ptr(scal), ptr(self.partials), beta_num, beta_den,
+                           ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials), beta_num, beta_den,
                            self.nty, self.ntz, _stream()), "fused_apply")
         _check(self._final(ptr(pb.latd), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
                            self.nty, self.ntz, self.sy, self.sz, _stream()), "fused_finalize")
