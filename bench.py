@@ -63,11 +63,20 @@ def main(argv=None) -> int:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {n}", file=sys.stderr)
     dtype = torch.float64 if bits == 64 else torch.float32
     nx = compute_mesh_size(dpg * n, degree)
+    def log(msg):
+        if comm.rank == 0:
+            print(f"[bench {time.perf_counter() - t_setup:8.2f}s] {msg}", file=sys.stderr,
+                  flush=True)
+
     t_setup = time.perf_counter()
+    log(f"mesh {nx} degree {degree} fp{bits} on {n} rank(s)")
     pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, 0.0)
+    log("problem built")
     u = pb.assemble_rhs()
     x = pb.new_vector()
+    log("rhs assembled")
     op = make_operator(pb, a.kernel, a.geometry)
+    log(f"operator {getattr(op, 'name', type(op).__name__)} ready")
     gpu = a.platform == "gpu"
 
     def sync():
@@ -82,6 +91,7 @@ def main(argv=None) -> int:
         cg.start(op, x, u)
         cg.iterate(a.warmup)
     sync()
+    log("warmup done")
     t_setup = time.perf_counter() - t_setup
     t0 = time.perf_counter()
     if gpu:
