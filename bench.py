@@ -132,6 +132,7 @@ def main(argv=None) -> int:
                 "per_gpu_gdofs": value / n,
                 "y_norm": ynorm,
                 "setup_s": t_setup,
+                "hiplib": os.path.basename(os.environ.get("BDX_HIP_LIB", "") or "libbdx_hip.so"),
             },
         }
         print(json.dumps(line), flush=True)

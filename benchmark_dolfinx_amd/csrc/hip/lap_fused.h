@@ -31,6 +31,32 @@
 
 enum { kFusedAction = 0, kFusedCG = 1 };
 
+#ifndef BDX_FAST_RCP
+#define BDX_FAST_RCP 0
+#endif
+#ifndef BDX_TAB_LDS
+#define BDX_TAB_LDS 0
+#endif
+#ifndef BDX_EXP_NOGEOM
+#define BDX_EXP_NOGEOM 0
+#endif
+
+// 1/x from the hardware reciprocal estimate + two Newton steps (full
+// precision for the normal, positive Jacobian determinants seen here) instead
+// of the IEEE division sequence (div_scale x2, rcp, 5 fma, div_fmas, div_fixup).
+__device__ __forceinline__ double fast_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ float fast_rcp(float x) {
+  float r = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, r, 1.0f);
+  return __builtin_fmaf(r, e, r);
+}
+
 // Scheduling fence between unrolled iterations: keeps the scheduler from
 // hoisting every LDS read of a fully unrolled stage to its top (which costs
 // hundreds of registers and occupancy).
@@ -329,7 +355,11 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     // inside the layer instead of pinning them for the whole x-march.
     int toff = 0;
     asm volatile("" : "+s"(toff));
+#if BDX_TAB_LDS
+    const T* __restrict__ gt = s_tab + toff;   // uniform rows as LDS broadcast reads
+#else
     const T* __restrict__ gt = tb.tab + toff;  // wave-uniform rows -> SMEM (kernarg)
+#endif
     const T* __restrict__ su = s_u[cur];
     const T* __restrict__ sX = s_X[cur];
 
@@ -457,7 +487,11 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
         const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
         const T det = J00 * K00 + J01 * K10 + J02 * K20;
+#if BDX_FAST_RCP
+        const T sc = kwyz * s_qw[NQ + q] * fast_rcp(det);
+#else
         const T sc = kwyz * s_qw[NQ + q] / det;
+#endif
         // h = K^T g, F = sc K h  (= kappa w det J^-1 J^-T g)
         const T h0 = K00 * gx[q] + K10 * gy[q] + K20 * gz[q];
         const T h1 = K01 * gx[q] + K11 * gy[q] + K21 * gz[q];
@@ -465,6 +499,11 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         fx = sc * (K00 * h0 + K01 * h1 + K02 * h2);
         fy = sc * (K10 * h0 + K11 * h1 + K12 * h2);
         fz = sc * (K20 * h0 + K21 * h1 + K22 * h2);
+#if BDX_EXP_NOGEOM  // timing experiment only: wrong numerics
+        fx = kwyz * gx[q];
+        fy = kwyz * gy[q];
+        fz = kwyz * gz[q];
+#endif
       } else {
         T Gd[6] = {0, 0, 0, 0, 0, 0};
         if (cell_on) {

@@ -1,0 +1,688 @@
+// Fused structured operator kernel, v2 ("fused2"): the same x-march /
+// (y, z)-tile / atomic-free design as lap_fused.h (and the same operator as
+// the reference's stiffness_operator_gpu + geometry_computation_gpu,
+// src/laplacian_gpu.hpp:91-426, src/geometry_gpu.hpp:26-132), re-engineered
+// for instruction economy after rocprofv3 showed v1 spending ~45 % of its
+// VALU issue on index arithmetic and SGPR spill traffic:
+//
+// * All per-element addressing is precomputed once per thread before the
+//   march: the input-staging elements, the output elements (their <= 4 LDS
+//   sources in the element-vector scratch, the destination class and a
+//   32-bit offset), and the vertex elements.  Per layer only 64-bit uniform
+//   base pointers advance (SGPRs), so the march body carries no 64-bit index
+//   math and no lattice struct.
+// * Dirichlet tests are per-thread bits for y/z (layer invariant) plus one
+//   compare against the local index of the global x boundary plane.
+// * 1/det uses the hardware reciprocal + two Newton steps.
+// * OTF geometry only (the stored-G layout stays on v1).
+//
+// Interface partials (YB/ZB/CB) and the finalize pass are those of v1.
+#pragma once
+#include "lap_fused.h"
+
+template <typename T>
+struct Fused2Args {
+  const T* __restrict__ u;     // action: input; CG: r
+  const T* __restrict__ pold;  // CG: previous p
+  T* __restrict__ pnew;        // CG: new p (tile-owned dofs)
+  T* __restrict__ y;
+  T* __restrict__ yb;
+  T* __restrict__ zb;
+  T* __restrict__ cb;
+  const T* __restrict__ xv;
+  const double* __restrict__ scal;
+  double* __restrict__ partials;
+  int64_t ps;      // x-plane stride of the vectors (Ly * ld)
+  int64_t ybps;    // x-plane strides of the interface buffers
+  int64_t zbps;
+  int64_t cbps;
+  int64_t vps;     // x-plane stride of the vertex array ((n1+1)(n2+1)*3)
+  int ncx, n1, n2;
+  int Ly, Lz, ld;
+  int ownx, owny, ownz;          // rank-owned extents (L - gh)
+  int bcx_lo, bcx_hi;            // local index of the global boundary plane, -1 if none
+  int bcy_lo, bcy_hi, bcz_lo, bcz_hi;
+  int nty, ntz;
+  int beta_num, beta_den;        // CG: beta = scal[num] / scal[den]; num < 0 -> 0
+  T kappa;
+};
+
+template <typename T, int ND, int NQ, int TY, int TZ, int MODE>
+__global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
+    lap_fused2_kernel(Fused2Args<T> A, FusedTables<T> tb) {
+  using S = FusedShape<T, ND, NQ, TY, TZ>;
+  constexpr int P = S::P, DY = S::DY, DZ = S::DZ, PL = DY * DZ;
+  constexpr int DZP = S::DZP, PLP = DY * DZP;
+  constexpr int NQ2 = NQ * NQ;
+  constexpr bool IDENT = (ND == NQ);
+  constexpr int NT = S::threads;
+  constexpr int NPF = (P * PL + NT - 1) / NT;     // staged input dofs per thread and layer
+  constexpr int NOUT = (ND * PL + NT - 1) / NT;   // output dofs per thread and layer
+  constexpr int NCP = (PL + NT - 1) / NT;         // carried-plane copies per thread
+  constexpr int NV = (TY + 1) * (TZ + 1) * 3;
+  constexpr int NPV = (NV + NT - 1) / NT;
+  constexpr int XP = S::XP, NP = S::NP;
+  constexpr int ZSLOT = S::work;                  // a zero row at the end of s_w2
+  static_assert(S::work + XP < 32768, "16-bit LDS source offsets");
+  static_assert(PL < 256, "8-bit plane index");
+
+  __shared__ __attribute__((aligned(16))) T s_tab[S::TAB];
+  __shared__ T s_qw[2 * NQ];
+  __shared__ T s_u[2][ND * PLP];
+  __shared__ T s_c[2][PL];
+  __shared__ __attribute__((aligned(16))) T s_w1[S::work];
+  __shared__ __attribute__((aligned(16))) T s_w2[S::work + XP];
+  __shared__ __attribute__((aligned(16))) T s_w3[S::work];
+  __shared__ T s_X[2][2 * NV];
+  __shared__ double s_red[16];
+
+  const int tid = threadIdx.x;
+  for (int i = tid; i < S::TAB; i += NT) s_tab[i] = tb.tab[i];
+  if (tid < NQ) {
+    s_qw[tid] = tb.qpts[tid];
+    s_qw[NQ + tid] = tb.wts[tid];
+  }
+  if (tid < XP) s_w2[ZSLOT + tid] = T(0);
+
+  // XCD-aware bijective remap of the block id (cdna_hip_programming.md T1).
+  const int nblk = gridDim.x, ob = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
+  const int ty = bid / A.ntz, tz = bid % A.ntz;
+  const int y0 = ty * TY * P, z0 = tz * TZ * P;
+  const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
+  const int ncx = A.ncx;
+  const bool top_y = (ty == A.nty - 1), top_z = (tz == A.ntz - 1);
+  const int ey = (y0 + DY <= Ly) ? DY : Ly - y0;
+  const int ez = (z0 + DZ <= Lz) ? DZ : Lz - z0;
+  const int oy = top_y ? ey : TY * P;
+  const int oz = top_z ? ez : TZ * P;
+
+  const int c = (tid / NQ2 < S::cells) ? tid / NQ2 : S::cells - 1;
+  const int a = (tid / NQ) % NQ, b = tid % NQ;
+  const int cy = c / TZ, cz = c % TZ;
+  const bool lane_on = tid < S::lanes;
+  const bool cell_on = lane_on && (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
+  const int ycell = cy * P, zcell = cz * P;
+  T* w1c = s_w1 + c * NQ2 * XP;
+  T* w2c = s_w2 + c * NQ2 * XP;
+  T* w3c = s_w3 + c * NQ2 * XP;
+
+  T beta = T(0);
+  if constexpr (MODE == kFusedCG) {
+    if (A.beta_num >= 0) beta = static_cast<T>(A.scal[A.beta_num] / A.scal[A.beta_den]);
+  }
+  double pap = 0.0;
+
+  // y/z classification of a slab position (layer invariant)
+  enum { kValid = 1, kOwnT = 2, kBcYZ = 4, kRownYZ = 8 };
+  auto yz_flags = [&](int ly, int lz) -> int {
+    if (ly >= ey || lz >= ez) return 0;
+    const int gy = y0 + ly, gz = z0 + lz;
+    int f = kValid;
+    if (ly < oy && lz < oz) f |= kOwnT;
+    if (gy == A.bcy_lo || gy == A.bcy_hi || gz == A.bcz_lo || gz == A.bcz_hi) f |= kBcYZ;
+    if (gy < A.owny && gz < A.ownz) f |= kRownYZ;
+    return f;
+  };
+  // Input value of a staged dof + its CG / Dirichlet side effects.
+  auto stage = [&](int f, int gx, const T* __restrict__ ul, T* __restrict__ pn, T* __restrict__ yl,
+                   int goff) -> T {
+    T v;
+    if constexpr (MODE == kFusedCG) {
+      v = ul[goff] + beta * A.pold[(ul - A.u) + goff];
+    } else {
+      v = ul[goff];
+    }
+    (void)pn;
+    if constexpr (MODE == kFusedCG) {
+      if (f & kOwnT) pn[goff] = v;
+    }
+    if ((f & kBcYZ) || gx == A.bcx_lo || gx == A.bcx_hi) {
+      if (f & kOwnT) {
+        const bool rown = (f & kRownYZ) && gx < A.ownx;
+        yl[goff] = rown ? v : T(0);
+        if constexpr (MODE == kFusedCG) {
+          if (rown) pap += static_cast<double>(v) * static_cast<double>(v);
+        }
+      }
+      v = T(0);
+    }
+    return v;
+  };
+
+  // ---- per-thread staging descriptors (planes 1..P of a layer)
+  int st_goff[NPF], st_meta[NPF];
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) {
+    const int e = tid + k * NT;
+    st_goff[k] = 0;
+    st_meta[k] = 0;
+    if (e < P * PL) {
+      const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      const int f = yz_flags(ly, lz);
+      st_goff[k] = (pl * Ly + y0 + ly) * ld + z0 + lz;
+      st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
+    }
+  }
+  // ---- per-thread output descriptors (planes 0..P of a layer)
+  int o_src[NOUT][2], o_off[NOUT], o_meta[NOUT];
+#pragma unroll
+  for (int k = 0; k < NOUT; ++k) {
+    const int e = tid + k * NT;
+    o_src[k][0] = o_src[k][1] = ZSLOT | (ZSLOT << 16);
+    o_off[k] = 0;
+    o_meta[k] = 0;
+    if (e < ND * PL) {
+      const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      const int f = yz_flags(ly, lz);
+      if (f & kValid) {
+        const int cyh = (ly / P < TY - 1) ? ly / P : TY - 1;
+        const int cyl = (ly % P == 0 && ly > 0 && ly / P - 1 < cyh) ? ly / P - 1 : cyh;
+        const int czh = (lz / P < TZ - 1) ? lz / P : TZ - 1;
+        const int czl = (lz % P == 0 && lz > 0 && lz / P - 1 < czh) ? lz / P - 1 : czh;
+        int src[4] = {ZSLOT, ZSLOT, ZSLOT, ZSLOT};
+        int ns = 0;
+        for (int ccy = cyl; ccy <= cyh; ++ccy)
+          for (int ccz = czl; ccz <= czh; ++ccz)
+            src[ns++] = (((ccy * TZ + ccz) * NQ + (ly - ccy * P)) * NQ + (lz - ccz * P)) * XP + pl;
+        o_src[k][0] = src[0] | (src[1] << 16);
+        o_src[k][1] = src[2] | (src[3] << 16);
+        const int gy = y0 + ly, gz = z0 + lz;
+        const bool iy = ly < oy, iz = lz < oz;
+        int kind, off;
+        if (iy && iz) {
+          kind = 0;
+          off = (pl * Ly + gy) * ld + gz;
+        } else if (!iy && iz) {
+          kind = 1;
+          off = static_cast<int>(pl * A.ybps) + ty * Lz + gz;
+        } else if (iy && !iz) {
+          kind = 2;
+          off = static_cast<int>(pl * A.zbps) + gy * (A.ntz - 1) + tz;
+        } else {
+          kind = 3;
+          off = static_cast<int>(pl * A.cbps) + ty * (A.ntz - 1) + tz;
+        }
+        o_off[k] = off;
+        o_meta[k] = f | (kind << 4) | (pl << 8) | (rem << 12);
+      }
+    }
+  }
+  // ---- carried-plane copy descriptors (plane P of a slab -> plane 0 of the next)
+  int cp_lds[NCP];
+#pragma unroll
+  for (int k = 0; k < NCP; ++k) {
+    const int e = tid + k * NT;
+    cp_lds[k] = (e < PL) ? (e / DZ) * DZP + e % DZ : -1;
+  }
+  // ---- vertex descriptors
+  int v_off[NPV];
+#pragma unroll
+  for (int k = 0; k < NPV; ++k) {
+    const int e = tid + k * NT;
+    v_off[k] = -1;
+    if (e < NV) {
+      const int d = e % 3, r = e / 3;
+      const int vz = r % (TZ + 1), vy = r / (TZ + 1);
+      const int gy = ty * TY + vy, gz = tz * TZ + vz;
+      if (gy <= A.n1 && gz <= A.n2) v_off[k] = (gy * (A.n2 + 1) + gz) * 3 + d;
+    }
+  }
+
+  // ---- prologue: layer 0 (planes 0..P), vertex planes 0/1, zero carry
+  for (int e = tid; e < ND * PL; e += NT) {
+    const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+    const int f = yz_flags(ly, lz);
+    T v = T(0);
+    if (f & kValid) v = stage(f, pl, A.u, A.pnew, A.y, (pl * Ly + y0 + ly) * ld + z0 + lz);
+    s_u[0][pl * PLP + ly * DZP + lz] = v;
+  }
+  for (int e = tid; e < 2 * NV; e += NT) {
+    const int k = e % NV;
+    int off = -1;
+    {
+      const int d = k % 3, r = k / 3;
+      const int vz = r % (TZ + 1), vy = r / (TZ + 1);
+      const int gy = ty * TY + vy, gz = tz * TZ + vz;
+      if (gy <= A.n1 && gz <= A.n2) off = (gy * (A.n2 + 1) + gz) * 3 + d;
+    }
+    s_X[0][e] = off >= 0 ? A.xv[(e / NV) * A.vps + off] : T(0);
+  }
+  for (int e = tid; e < PL; e += NT) s_c[0][e] = T(0);
+
+  T Js[3] = {0, 0, 0};
+  T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};
+  T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};
+
+  for (int cx = 0; cx < ncx; ++cx) {
+    const int cur = cx & 1, nxt = cur ^ 1;
+    const bool last = (cx == ncx - 1);
+    __syncthreads();
+
+    // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
+    const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
+    T pf_r[NPF], pf_p[NPF];
+    T pf_v[NPV];
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      pf_r[k] = T(0);
+      pf_p[k] = T(0);
+      if (!last && (st_meta[k] & kValid)) {
+        pf_r[k] = A.u[lnext + st_goff[k]];
+        if constexpr (MODE == kFusedCG) pf_p[k] = A.pold[lnext + st_goff[k]];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPV; ++k) {
+      pf_v[k] = T(0);
+      if (!last && v_off[k] >= 0) pf_v[k] = A.xv[static_cast<int64_t>(cx + 2) * A.vps + v_off[k]];
+    }
+
+    int toff = 0;
+    asm volatile("" : "+s"(toff));
+    const T* __restrict__ gt = tb.tab + toff;
+    const T* __restrict__ su = s_u[cur];
+    const T* __restrict__ sX = s_X[cur];
+
+    const T* __restrict__ ua = su + (ycell + a) * DZP + zcell;
+    T* __restrict__ w1ab = w1c + (a * NQ + b) * XP;
+    T* __restrict__ w2ab = w2c + (a * NQ + b) * XP;
+    T* __restrict__ w3ab = w3c + (a * NQ + b) * XP;
+    const T* __restrict__ w1b = w1c + b * XP;
+    const T* __restrict__ w2b = w2c + b * XP;
+    const T* __restrict__ w1a = w1c + a * NQ * XP;
+    const T* __restrict__ w2a = w2c + a * NQ * XP;
+    const T* __restrict__ w3a = w3c + a * NQ * XP;
+
+    // ------------------------------------------------ interpolate to qpts
+    T U[NQ];
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[i * PLP + b] : T(0);
+    } else {
+      if (lane_on && a < ND) {
+        const T* __restrict__ ph = s_tab + S::OFF_PR + b * NP;
+        T o[ND];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) o[i] = 0;
+#pragma unroll 1
+        for (int k = 0; k < ND; ++k) {
+          const T cc = ph[k];
+#pragma unroll
+          for (int i = 0; i < ND; ++i) o[i] += cc * ua[i * PLP + k];
+        }
+        strow<ND>(w1ab, o);
+      }
+      __syncthreads();
+      const T* __restrict__ pa = s_tab + S::OFF_PR + a * NP;
+      T t2[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) t2[i] = 0;
+#pragma unroll 1
+      for (int j = 0; j < ND; ++j) {
+        T row[ND];
+        ldrow<ND>(w1b + j * NQ * XP, row);
+        const T cc = pa[j];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) t2[i] += cc * row[i];
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) U[q] = 0;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) U[q] += gt[S::OFF_PC + i * XP + q] * t2[i];
+      }
+    }
+
+    // ------------------------------------------------ reference gradient
+    if (lane_on) strow<NQ>(w2ab, U);
+    __syncthreads();
+    T gx[NQ], gy[NQ], gz[NQ];
+    {
+      const T* __restrict__ dra = s_tab + S::OFF_DR + a * XP;
+      const T* __restrict__ drb = s_tab + S::OFF_DR + b * XP;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) gx[q] = gy[q] = gz[q] = 0;
+#pragma unroll 1
+      for (int m = 0; m < NQ; ++m) {
+        T ry[NQ], rz[NQ];
+        ldrow<NQ>(w2b + m * NQ * XP, ry);
+        ldrow<NQ>(w2a + m * XP, rz);
+        const T um = w2ab[m], cy_ = dra[m], cz_ = drb[m];
+        const T* __restrict__ dc = gt + S::OFF_DC + m * XP;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          gx[q] += dc[q] * um;
+          gy[q] += cy_ * ry[q];
+          gz[q] += cz_ * rz[q];
+        }
+      }
+    }
+
+    // ------------------------------------------------ geometry coefficients
+    {
+      const T t = s_qw[a], uu = s_qw[b];
+      const T* X0 = sX;
+      const T* X1 = sX + NV;
+      const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
+      const int v10 = v00 + (TZ + 1) * 3, v11 = v10 + 3;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const T X000 = X0[v00 + d], X001 = X0[v01 + d], X010 = X0[v10 + d], X011 = X0[v11 + d];
+        const T X100 = X1[v00 + d], X101 = X1[v01 + d], X110 = X1[v10 + d], X111 = X1[v11 + d];
+        Js[d] = (1 - t) * ((1 - uu) * (X100 - X000) + uu * (X101 - X001)) +
+                t * ((1 - uu) * (X110 - X010) + uu * (X111 - X011));
+        Jt0[d] = (1 - uu) * (X010 - X000) + uu * (X011 - X001);
+        Jt1[d] = (1 - uu) * (X110 - X100) + uu * (X111 - X101) - Jt0[d];
+        Ju0[d] = (1 - t) * (X001 - X000) + t * (X011 - X010);
+        Ju1[d] = (1 - t) * (X101 - X100) + t * (X111 - X110) - Ju0[d];
+      }
+    }
+    const T kwyz = A.kappa * s_qw[NQ + a] * s_qw[NQ + b];
+
+    // ------------------------------------------------ F = kappa G grad
+    T Fx[NQ];
+    using V = typename VecOf<T>::type;
+    constexpr int VW = VecOf<T>::W;
+    V vy, vz;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const T s = s_qw[q];
+      const T J00 = Js[0], J10 = Js[1], J20 = Js[2];
+      const T J01 = Jt0[0] + s * Jt1[0], J11 = Jt0[1] + s * Jt1[1], J21 = Jt0[2] + s * Jt1[2];
+      const T J02 = Ju0[0] + s * Ju1[0], J12 = Ju0[1] + s * Ju1[1], J22 = Ju0[2] + s * Ju1[2];
+      const T K00 = J11 * J22 - J12 * J21, K01 = J02 * J21 - J01 * J22, K02 = J01 * J12 - J02 * J11;
+      const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
+      const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
+      const T det = J00 * K00 + J01 * K10 + J02 * K20;
+      const T sc = kwyz * s_qw[NQ + q] * fast_rcp(det);
+      const T h0 = K00 * gx[q] + K10 * gy[q] + K20 * gz[q];
+      const T h1 = K01 * gx[q] + K11 * gy[q] + K21 * gz[q];
+      const T h2 = K02 * gx[q] + K12 * gy[q] + K22 * gz[q];
+      T fx = sc * (K00 * h0 + K01 * h1 + K02 * h2);
+      T fy = sc * (K10 * h0 + K11 * h1 + K12 * h2);
+      T fz = sc * (K20 * h0 + K21 * h1 + K22 * h2);
+      BDX_PIN3(fx, fy, fz);
+      Fx[q] = fx;
+      vy[q % VW] = fy;
+      vz[q % VW] = fz;
+      if (q % VW == VW - 1 || q == NQ - 1) {
+        if (q % VW != VW - 1) {
+#pragma unroll
+          for (int e = q % VW + 1; e < VW; ++e) vy[e] = vz[e] = T(0);
+        }
+        if (lane_on) {
+          *reinterpret_cast<V*>(w1ab + (q / VW) * VW) = vy;
+          *reinterpret_cast<V*>(w3ab + (q / VW) * VW) = vz;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ------------------------------------------------ transposed gradient
+    T r[NQ];
+    {
+      if (lane_on) strow<NQ>(w2ab, Fx);
+      const T* __restrict__ dca = s_tab + S::OFF_DC + a * XP;
+      const T* __restrict__ dcb = s_tab + S::OFF_DC + b * XP;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) r[q] = 0;
+#pragma unroll 1
+      for (int m = 0; m < NQ; ++m) {
+        T r1[NQ], r3[NQ];
+        ldrow<NQ>(w1b + m * NQ * XP, r1);
+        ldrow<NQ>(w3a + m * XP, r3);
+        const T fm = w2ab[m], ca = dca[m], cb_ = dcb[m];
+        const T* __restrict__ dr = gt + S::OFF_DR + m * XP;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) r[q] += dr[q] * fm + ca * r1[q] + cb_ * r3[q];
+      }
+    }
+    T sx[ND];
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) sx[i] = r[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        T acc = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc += gt[S::OFF_PC + i * XP + q] * r[q];
+        sx[i] = acc;
+      }
+    }
+
+    // ------------------------------------------------ back to the dofs
+    T ye[ND];
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) ye[i] = sx[i];
+    } else {
+      __syncthreads();
+      if (lane_on) strow<ND>(w2ab, sx);
+      __syncthreads();
+      if (lane_on && a < ND) {
+        const T* __restrict__ pca = s_tab + S::OFF_PC + a * XP;
+        T o[ND];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) o[i] = 0;
+#pragma unroll 1
+        for (int q = 0; q < NQ; ++q) {
+          T row[ND];
+          ldrow<ND>(w2b + q * NQ * XP, row);
+          const T cc = pca[q];
+#pragma unroll
+          for (int i = 0; i < ND; ++i) o[i] += cc * row[i];
+        }
+        strow<ND>(w1ab, o);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < ND; ++i) ye[i] = 0;
+      if (a < ND && b < ND) {
+        const T* __restrict__ pcb = s_tab + S::OFF_PC + b * XP;
+#pragma unroll 1
+        for (int q = 0; q < NQ; ++q) {
+          T row[ND];
+          ldrow<ND>(w1a + q * XP, row);
+          const T cc = pcb[q];
+#pragma unroll
+          for (int i = 0; i < ND; ++i) ye[i] += cc * row[i];
+        }
+      }
+    }
+
+    // ------------------------------------------------ element vectors -> LDS
+    const bool dof_lane = cell_on && a < ND && b < ND;
+    if constexpr (MODE == kFusedCG) {
+      if (dof_lane) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          pap += static_cast<double>(ua[i * PLP + b]) * static_cast<double>(ye[i]);
+      }
+    }
+    if constexpr (IDENT) {
+      __syncthreads();
+    }
+    if (lane_on && a < ND && b < ND) {
+      if (!dof_lane) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) ye[i] = T(0);
+      }
+      strow<ND>(w2ab, ye);
+    }
+    __syncthreads();
+
+    // ------------------------------------------------ gather-sum and write out
+    {
+      const int64_t lbase = static_cast<int64_t>(cx) * P;
+      T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
+                                  A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
+#pragma unroll
+      for (int k = 0; k < NOUT; ++k) {
+        const int m = o_meta[k];
+        if (!(m & kValid)) continue;
+        const int pl = (m >> 8) & 15, rem = m >> 12;
+        T v = s_w2[o_src[k][0] & 0xffff] + s_w2[o_src[k][0] >> 16] +
+              s_w2[o_src[k][1] & 0xffff] + s_w2[o_src[k][1] >> 16];
+        if (pl == 0) v += s_c[cur][rem];
+        if (pl == P && !last) {
+          s_c[nxt][rem] = v;
+          continue;
+        }
+        const int gxx = cx * P + pl;
+        const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
+        const int kind = (m >> 4) & 3;
+        if (bc) {
+          if (kind == 0) continue;  // Dirichlet y was written at staging
+          v = T(0);
+        }
+        T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
+        dst[o_off[k]] = v;
+      }
+    }
+
+    // ------------------------------------------------ stage the next layer
+    if (!last) {
+      T* __restrict__ un = s_u[nxt];
+#pragma unroll
+      for (int k = 0; k < NCP; ++k)
+        if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
+      T* __restrict__ pnl = A.pnew + lnext;
+      T* __restrict__ yl = A.y + lnext;
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) {
+        const int m = st_meta[k];
+        if (tid + k * NT < P * PL) {
+          T v = T(0);
+          if (m & kValid) {
+            const int gxx = (cx + 1) * P + ((m >> 4) & 15);
+            T val;
+            if constexpr (MODE == kFusedCG) {
+              val = pf_r[k] + beta * pf_p[k];
+            } else {
+              val = pf_r[k];
+            }
+            if constexpr (MODE == kFusedCG) {
+              if (m & kOwnT) pnl[st_goff[k]] = val;
+            }
+            if ((m & kBcYZ) || gxx == A.bcx_hi) {
+              if (m & kOwnT) {
+                const bool rown = (m & kRownYZ) && gxx < A.ownx;
+                yl[st_goff[k]] = rown ? val : T(0);
+                if constexpr (MODE == kFusedCG) {
+                  if (rown) pap += static_cast<double>(val) * static_cast<double>(val);
+                }
+              }
+              val = T(0);
+            }
+            v = val;
+          }
+          un[m >> 8] = v;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NPV; ++k) {
+        const int e = tid + k * NT;
+        if (e < NV) s_X[nxt][e] = sX[NV + e];
+      }
+#pragma unroll
+      for (int k = 0; k < NPV; ++k) {
+        const int e = tid + k * NT;
+        if (e < NV) s_X[nxt][NV + e] = pf_v[k];
+      }
+    }
+  }
+  if constexpr (MODE == kFusedCG) {
+    const double t = block_sum(pap, s_red);
+    if (tid == 0) A.partials[blockIdx.x] = t;
+  }
+}
+
+// Host-side launch: build the argument block from the packed lattice
+// descriptor (fem/mesh.py LocalLattice.as_int64) and launch one workgroup per
+// (y, z) tile.
+template <typename T, int ND, int NQ, int MODE>
+int launch_fused2(const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
+  using TF = TileFor<NQ>;
+  using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
+  const int nblk = a.nty * a.ntz;
+  if (nblk <= 0) return 0;
+  lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE><<<nblk, S::threads, 0, st>>>(a, tb);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <typename T>
+inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int ntz) {
+  const BdxLattice L = BdxLattice::from(latd);
+  const int64_t P = L.P;
+  // 32-bit per-layer offsets: one layer of the vector must be < 2^31 elements
+  if ((P + 1) * L.L[1] * L.ld >= (int64_t(1) << 31)) return static_cast<int>(hipErrorInvalidValue);
+  a.ps = L.L[1] * L.ld;
+  a.ybps = static_cast<int64_t>(nty - 1) * L.L[2];
+  a.zbps = L.L[1] * static_cast<int64_t>(ntz - 1);
+  a.cbps = static_cast<int64_t>(nty - 1) * (ntz - 1);
+  a.vps = (L.n[1] + 1) * (L.n[2] + 1) * 3;
+  a.ncx = static_cast<int>(L.n[0]);
+  a.n1 = static_cast<int>(L.n[1]);
+  a.n2 = static_cast<int>(L.n[2]);
+  a.Ly = static_cast<int>(L.L[1]);
+  a.Lz = static_cast<int>(L.L[2]);
+  a.ld = static_cast<int>(L.ld);
+  a.ownx = static_cast<int>(L.L[0] - L.gh[0]);
+  a.owny = static_cast<int>(L.L[1] - L.gh[1]);
+  a.ownz = static_cast<int>(L.L[2] - L.gh[2]);
+  auto lo = [&](int d) { return L.g0[d] == 0 ? 0 : -1; };
+  auto hi = [&](int d) {
+    const int64_t i = L.N[d] - 1 - L.g0[d];
+    return (i >= 0 && i < L.L[d]) ? static_cast<int>(i) : -1;
+  };
+  a.bcx_lo = lo(0);
+  a.bcx_hi = hi(0);
+  a.bcy_lo = lo(1);
+  a.bcy_hi = hi(1);
+  a.bcz_lo = lo(2);
+  a.bcz_hi = hi(2);
+  a.nty = nty;
+  a.ntz = ntz;
+  return 0;
+}
+
+#define BDX_FUSED2_TU(T, SUF, PP)                                                   \
+  extern "C" int bdx_fused2_apply_##SUF##_p##PP(                                   \
+      int mode, const int64_t* latd, int nq, const double* wts, const double* qpts, \
+      const T* u, const T* pold, T* pnew, T* y, T* yb, T* zb, T* cb, const T* xv,  \
+      const T* tabs, double kappa, const double* scal, double* partials,           \
+      int beta_num, int beta_den, int nty, int ntz, hipStream_t st) {              \
+    Fused2Args<T> a;                                                               \
+    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));       \
+    a.u = u;                                                                       \
+    a.pold = pold;                                                                 \
+    a.pnew = pnew;                                                                 \
+    a.y = y;                                                                       \
+    a.yb = yb;                                                                     \
+    a.zb = zb;                                                                     \
+    a.cb = cb;                                                                     \
+    a.xv = xv;                                                                     \
+    a.scal = scal;                                                                 \
+    a.partials = partials;                                                         \
+    a.beta_num = beta_num;                                                         \
+    a.beta_den = beta_den;                                                         \
+    a.kappa = static_cast<T>(kappa);                                               \
+    if (!tabs) return static_cast<int>(hipErrorInvalidValue);                      \
+    FusedTables<T> tb;                                                             \
+    for (int i = 0; i < kFusedTabMax; ++i) tb.tab[i] = tabs[i];                    \
+    for (int q = 0; q < kMaxNq; ++q) {                                             \
+      tb.qpts[q] = q < nq ? static_cast<T>(qpts[q]) : T(0);                        \
+      tb.wts[q] = q < nq ? static_cast<T>(wts[q]) : T(0);                          \
+    }                                                                              \
+    if (nq == PP + 1)                                                              \
+      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 1, kFusedCG>(a, tb, st) \
+                              : launch_fused2<T, PP + 1, PP + 1, kFusedAction>(a, tb, st); \
+    if (nq == PP + 2)                                                              \
+      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 2, kFusedCG>(a, tb, st) \
+                              : launch_fused2<T, PP + 1, PP + 2, kFusedAction>(a, tb, st); \
+    return static_cast<int>(hipErrorInvalidValue);                                 \
+  }

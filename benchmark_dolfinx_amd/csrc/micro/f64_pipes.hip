@@ -1,0 +1,86 @@
+// Microbenchmark: does the FP64 MFMA pipe run concurrently with FP64 VALU
+// FMAs on gfx950?  Three kernels of equal per-wave work:
+//   valu: every wave runs independent v_fma_f64 chains
+//   mfma: every wave runs v_mfma_f64_16x16x4_f64 on 4 independent accumulators
+//   mix : waves 0-3 of a 512-thread workgroup run the VALU loop, waves 4-7 the
+//         MFMA loop (so each SIMD hosts one of each).
+// Build: hipcc --offload-arch=gfx950 -O3 f64_pipes.hip -o /tmp/f64_pipes
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <chrono>
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double valu_loop(int iters, double x) {
+  double a0 = x, a1 = x + 1, a2 = x + 2, a3 = x + 3, a4 = x + 4, a5 = x + 5, a6 = x + 6, a7 = x + 7;
+  const double m = 0.999999, c = 1e-7;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a0 = fma(a0, m, c); a1 = fma(a1, m, c); a2 = fma(a2, m, c); a3 = fma(a3, m, c);
+      a4 = fma(a4, m, c); a5 = fma(a5, m, c); a6 = fma(a6, m, c); a7 = fma(a7, m, c);
+    }
+  }
+  return a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+__device__ __forceinline__ double mfma_loop(int iters, double x) {
+  d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+  double a = x, b = 1.0 - x;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
+    }
+  }
+  d4 s = c0 + c1 + c2 + c3;
+  return s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ void __launch_bounds__(512) k_valu(int it, double* out) {
+  double r = valu_loop(it, threadIdx.x * 1e-3);
+  if (r == 12345.0) out[0] = r;
+}
+__global__ void __launch_bounds__(512) k_mfma(int it, double* out) {
+  double r = mfma_loop(it, threadIdx.x * 1e-3);
+  if (r == 12345.0) out[0] = r;
+}
+__global__ void __launch_bounds__(512) k_mix(int itv, int itm, double* out) {
+  double r;
+  if (threadIdx.x < 256) r = valu_loop(itv, threadIdx.x * 1e-3);
+  else r = mfma_loop(itm, threadIdx.x * 1e-3);
+  if (r == 12345.0) out[0] = r;
+}
+
+template <typename F>
+double timeit(F f) {
+  f();
+  hipDeviceSynchronize();
+  auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < 5; ++r) f();
+  hipDeviceSynchronize();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / 5;
+}
+
+int main() {
+  double* out;
+  hipMalloc(&out, 8);
+  const int blocks = 256 * 4;
+  const int itv = 2000, itm = 1000;
+  // FLOPs: valu per wave-iter: 64 fma * 64 lanes * 2; mfma per wave-iter: 16 mfma * 2048
+  const double fv = 2.0 * 64 * 64 * itv, fm = 16.0 * 2048 * itm;  // per wave
+  double tv = timeit([&] { k_valu<<<blocks, 512>>>(itv, out); });
+  double tm = timeit([&] { k_mfma<<<blocks, 512>>>(itm, out); });
+  double tx = timeit([&] { k_mix<<<blocks, 512>>>(itv, itm, out); });
+  const double waves = blocks * 8.0;
+  printf("valu: %.3f ms  %.1f TF/s\n", tv * 1e3, waves * fv / tv / 1e12);
+  printf("mfma: %.3f ms  %.1f TF/s\n", tm * 1e3, waves * fm / tm / 1e12);
+  printf("mix : %.3f ms  %.1f TF/s (half waves each: valu %.1f + mfma %.1f)\n", tx * 1e3,
+         waves / 2 * (fv + fm) / tx / 1e12, waves / 2 * fv / tx / 1e12, waves / 2 * fm / tx / 1e12);
+  printf("(if concurrent: mix ~= max(valu, mfma)/2 of the pure times = %.3f ms; if shared: sum/2 = %.3f ms)\n",
+         0.5 * (tv > tm ? tv : tm) * 1e3, 0.5 * (tv + tm) * 1e3);
+  return 0;
+}

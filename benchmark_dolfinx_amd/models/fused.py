@@ -27,19 +27,25 @@ from ..ops.native import ptr
 from ..utils.timing import timed
 
 
-def fused_supported(pb) -> bool:
+def fused_supported(pb, version: int = 1) -> bool:
     if pb.platform != "gpu":
         return False
     lib = native.hip()
-    return hasattr(lib, f"bdx_fused_apply_{pb.suf}_p{pb.degree}")
+    v = "" if version == 1 else str(version)
+    return hasattr(lib, f"bdx_fused{v}_apply_{pb.suf}_p{pb.degree}")
 
 
 class FusedLaplacianGPU:
-    name = "fused"
+    """version=1: lap_fused.h (OTF or stored G); version=2: lap_fused2.h
+    (OTF only, precomputed per-thread addressing)."""
 
-    def __init__(self, pb, geometry: str = "otf"):
+    def __init__(self, pb, geometry: str = "otf", version: int = 1):
         if geometry not in ("otf", "stored"):
             raise ValueError(f"unknown geometry mode {geometry}")
+        if version == 2 and geometry != "otf":
+            raise ValueError("fused2 supports on-the-fly geometry only")
+        self.version = version
+        self.name = "fused" if version == 1 else "fused2"
         self.pb = pb
         self.geometry = geometry
         self.lib = native.hip()
@@ -74,6 +80,8 @@ class FusedLaplacianGPU:
         ftab(t.nd, t.nq, ptr(t.phi0), ptr(t.dphi1), ptr(host))
         self.tabs = host  # host memory: copied into the kernel arguments
         self._apply = getattr(self.lib, f"bdx_fused_apply_{pb.suf}_p{P}")
+        if version == 2:
+            self._apply2 = getattr(self.lib, f"bdx_fused2_apply_{pb.suf}_p{P}")
         self._final = getattr(self.lib, f"bdx_fused_finalize_{pb.suf}")
         self.geom_code = 1 if geometry == "otf" else 0
         self.p_old = None
@@ -82,6 +90,15 @@ class FusedLaplacianGPU:
     # ------------------------------------------------------------ launches
     def _launch(self, mode, u, pold, pnew, y, scal=None, beta_num=-1, beta_den=-1):
         pb, t = self.pb, self.t
+        if self.version == 2:
+            _check(self._apply2(mode, ptr(pb.latd), t.nq, ptr(t.wts), ptr(t.qpts), ptr(u),
+                                ptr(pold), ptr(pnew), ptr(y), ptr(self.yb), ptr(self.zb),
+                                ptr(self.cb), ptr(pb.xv), ptr(self.tabs), pb.kappa, ptr(scal),
+                                ptr(self.partials), beta_num, beta_den, self.nty, self.ntz,
+                                _stream()), "fused2_apply")
+            _check(self._final(ptr(pb.latd), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
+                               self.nty, self.ntz, self.sy, self.sz, _stream()), "fused_finalize")
+            return
         _check(self._apply(self.geom_code, mode, ptr(pb.latd), t.nq, ptr(t.phi0), ptr(t.dphi1),
                            ptr(t.wts), ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(y),
                            ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(self.G), ptr(pb.xv),

@@ -88,19 +88,24 @@ def hip_flags() -> list[str]:
             "-I", str(CSRC / "include"), "-I", str(CSRC / "hip")]
 
 
-def build_hip(force: bool = False, jobs: int | None = None) -> Path:
+def build_hip(force: bool = False, jobs: int | None = None,
+              extra_flags: list[str] | None = None, variant: str = "") -> Path:
+    """Build libbdx_hip.so (or, with `variant`, libbdx_hip_<variant>.so with
+    `extra_flags` appended: used for A/B kernel experiments on the GPU box)."""
     srcs = _sources("hip", ".hip")
-    flags = hip_flags()
+    flags = hip_flags() + list(extra_flags or [])
+    out_so = HIP_SO if not variant else HERE / f"libbdx_hip_{variant}.so"
+    obj_dir = OBJ_DIR if not variant else OBJ_DIR / variant
     digest = _digest(srcs + _headers(), " ".join(flags))
-    if not force and _up_to_date(HIP_SO, digest):
-        return HIP_SO
+    if not force and _up_to_date(out_so, digest):
+        return out_so
     if not Path(HIPCC).exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
-    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    obj_dir.mkdir(parents=True, exist_ok=True)
     jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(srcs)))
 
     def compile_one(src: Path) -> Path:
-        obj = OBJ_DIR / (src.stem + ".o")
+        obj = obj_dir / (src.stem + ".o")
         odig = _digest([src] + _headers(), " ".join(flags))
         if not force and _up_to_date(obj, odig):
             return obj
@@ -110,12 +115,12 @@ def build_hip(force: bool = False, jobs: int | None = None) -> Path:
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = HIP_SO.with_suffix(".so.tmp")
+    tmp = out_so.with_suffix(".so.tmp")
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={HIP_ARCH}", *map(str, objs),
           "-o", str(tmp)])
-    os.replace(tmp, HIP_SO)
-    _stamp(HIP_SO, digest)
-    return HIP_SO
+    os.replace(tmp, out_so)
+    _stamp(out_so, digest)
+    return out_so
 
 
 def main(argv=None) -> int:
@@ -124,7 +129,14 @@ def main(argv=None) -> int:
     ap.add_argument("--hip", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--variant", action="append", default=[],
+                    help="NAME=FLAGS: also build libbdx_hip_NAME.so with extra hipcc flags")
     a = ap.parse_args(argv)
+    for v in a.variant:
+        name, _, fl = v.partition("=")
+        print("built", build_hip(a.force, a.jobs, fl.split(), name))
+    if a.variant and not (a.host or a.hip):
+        return 0
     both = not (a.host or a.hip)
     if a.host or both:
         print("built", build_host(a.force))

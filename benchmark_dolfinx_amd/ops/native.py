@@ -22,6 +22,7 @@ from . import build as _build
 _lock = threading.Lock()
 _host = None
 _hip = None
+_loaded = {}
 
 vp = ctypes.c_void_p
 i32 = ctypes.c_int
@@ -86,8 +87,10 @@ def hip():
     with _lock:
         if _hip is None:
             import torch  # noqa: F401  (shares the HIP runtime; see module doc)
-            path = _build.build_hip()
+            override = os.environ.get("BDX_HIP_LIB")  # A/B experiments: a variant .so
+            path = override if override else _build.build_hip()
             lib = ctypes.CDLL(str(path), mode=os.RTLD_NOW | ctypes.RTLD_GLOBAL)
+            _loaded["hip"] = str(path)
             from . import hip_api
             hip_api.declare(lib)
             _hip = lib
@@ -99,5 +102,5 @@ def loaded_libraries() -> list[str]:
     if _host is not None:
         out.append(str(_build.HOST_SO))
     if _hip is not None:
-        out.append(str(_build.HIP_SO))
+        out.append(_loaded.get("hip", str(_build.HIP_SO)))
     return out

@@ -1,0 +1,14 @@
+#!/bin/bash
+source scripts/gpu_steps.sh
+step pytest_fused 600 python -m pytest tests/test_gpu_fused.py -x -q
+for c in q3 q6; do
+  step bench_${c}_f1 300 python -u bench.py --steps 20 --warmup 3 --config $c --kernel fused
+  step bench_${c}_f2 300 python -u bench.py --steps 20 --warmup 3 --config $c --kernel fused2
+  step bench_${c}_f2w2 300 env BDX_HIP_LIB=$PWD/benchmark_dolfinx_amd/ops/libbdx_hip_w2.so python -u bench.py --steps 20 --warmup 3 --config $c --kernel fused2
+done
+step prof_f2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_f2 -o trace -- python3 bench.py --steps 10 --warmup 2 --config q3 --kernel fused2
+grep -h '^{' gpurun_out/bench_*.log | python -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['config']['model'][:3], d['config']['kernel'], d['config'].get('hiplib', ''), round(d['value'], 3), round(d['ms_per_step'], 3))
+" || true

@@ -38,9 +38,12 @@ def _tol(dt):
     return 1e-12 if dt == torch.float64 else 3e-5
 
 
-@pytest.mark.parametrize("geometry", ["otf", "stored"])
+VARIANTS = [("otf", 1), ("stored", 1), ("otf", 2)]
+
+
+@pytest.mark.parametrize("geometry,version", VARIANTS)
 @pytest.mark.parametrize("nc,P,qm,g,pert,dt", CASES)
-def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry):
+def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry, version):
     gpu = PoissonProblem(Comm(), nc, P, qm, g, dt, "gpu", pert)
     cpu = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "cpu", pert)
     rng = np.random.default_rng(3)
@@ -48,7 +51,7 @@ def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry):
     yc = cpu.new_vector()
     MatFreeLaplacianCPU(cpu).apply(u64, yc)
     yg = torch.full(gpu.lat.shape, float("nan"), dtype=dt, device=gpu.device)
-    FusedLaplacianGPU(gpu, geometry).apply(u64.to(gpu.device, dt), yg)
+    FusedLaplacianGPU(gpu, geometry, version).apply(u64.to(gpu.device, dt), yg)
     yg = yg.double().cpu()
     o = cpu.owned
     assert torch.isfinite(o(yg)).all()
@@ -56,24 +59,24 @@ def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry):
     assert err <= _tol(dt) * 50 * max(1.0, yc.abs().max().item()), err
 
 
-@pytest.mark.parametrize("geometry", ["otf", "stored"])
-def test_fused_cg_matches_host_cg(geometry):
+@pytest.mark.parametrize("geometry,version", VARIANTS)
+def test_fused_cg_matches_host_cg(geometry, version):
     nc = (5, 7, 11)
     gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", 0.1)
     cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", 0.1)
     xg = gpu.new_vector()
-    DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, geometry), xg, gpu.assemble_rhs(), 30)
+    DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, geometry, version), xg, gpu.assemble_rhs(), 30)
     xc = cpu.new_vector()
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 30)
     rel = (cpu.owned(xg.cpu()) - cpu.owned(xc)).abs().max().item() / xc.abs().max().item()
     assert rel < 1e-10, rel
 
 
-def _cg_job(comm, nc, P, nreps, geometry):
+def _cg_job(comm, nc, P, nreps, geometry, version=1):
     pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", 0.1)
     u = pb.assemble_rhs()
     x = pb.new_vector()
-    op = FusedLaplacianGPU(pb, geometry)
+    op = FusedLaplacianGPU(pb, geometry, version)
     DeviceCG(pb).solve(op, x, u, nreps)
     y = pb.new_vector()
     op.apply(u, y)
@@ -81,25 +84,27 @@ def _cg_job(comm, nc, P, nreps, geometry):
     return pb.norm(u), pb.norm(x), pb.norm(y)
 
 
+@pytest.mark.parametrize("version", [1, 2])
 @pytest.mark.parametrize("ranks", [2, 4, 8])
-def test_fused_partition_invariance_threaded(ranks):
-    ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf")[0]
-    got = run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf")
+def test_fused_partition_invariance_threaded(ranks, version):
+    ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version)[0]
+    got = run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf", version)
     for r in got:
         for a, b in zip(r, ref):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
 
 
-def test_fused_golden_and_mat_comp_16():
+@pytest.mark.parametrize("version", [1, 2])
+def test_fused_golden_and_mat_comp_16(version):
     nx = compute_mesh_size(1000, 3)
     pb = PoissonProblem(Comm(), nx, 3, 0, False, torch.float64, "gpu")
     u = pb.assemble_rhs()
     y = pb.new_vector()
-    FusedLaplacianGPU(pb).apply(u, y)
+    FusedLaplacianGPU(pb, "otf", version).apply(u, y)
     assert abs(pb.norm(y) - 9.912865833415553) < 1e-12
     nx = compute_mesh_size(100000, 3)
     pb = PoissonProblem(Comm(), nx, 3, 1, False, torch.float64, "gpu")
     u = pb.assemble_rhs()
     y = pb.new_vector()
-    FusedLaplacianGPU(pb).apply(u, y)
+    FusedLaplacianGPU(pb, "otf", version).apply(u, y)
     assert abs(pb.norm(y) - 0.14150257625641838) < 1e-13
