@@ -56,8 +56,10 @@ def build_parser() -> argparse.ArgumentParser:
     # MI355X extensions
     ap.add_argument("--kernel", default="auto", choices=["auto", "fused2", "fused", "v1"],
                     help="GPU operator kernel: fused structured kernel or the generic v1")
-    ap.add_argument("--geometry", default="auto", choices=["auto", "otf", "stored"],
-                    help="Geometry factors on the fly (otf) or precomputed (stored)")
+    ap.add_argument("--geometry", default="auto", choices=["auto", "otf", "otf-general", "stored"],
+                    help="Geometry factors on the fly (otf: constant-Jacobian fast path for "
+                         "parallelepiped cells; otf-general: always the trilinear path) or "
+                         "precomputed (stored, the reference's layout)")
     ap.add_argument("--warmup", type=int, default=0,
                     help="Untimed repetitions before the timed loop")
     return ap

@@ -47,7 +47,7 @@ struct Fused2Args {
   T kappa;
 };
 
-template <typename T, int ND, int NQ, int TY, int TZ, int MODE>
+template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
 __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
     lap_fused2_kernel(Fused2Args<T> A, FusedTables<T> tb) {
   using S = FusedShape<T, ND, NQ, TY, TZ>;
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   }
   for (int e = tid; e < PL; e += NT) s_c[0][e] = T(0);
 
-  T Js[3] = {0, 0, 0};
+  T Js[3] = {0, 0, 0};                        // AFF = 0 only
   T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};
   T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};
 
@@ -362,48 +362,65 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     }
 
     // ------------------------------------------------ geometry coefficients
+    // AFF = 0: general trilinear map, dX/ds = Js (constant along the thread's
+    // x column), dX/dt = Jt0 + s Jt1, dX/du = Ju0 + s Ju1, G formed per point.
+    // AFF = 1: every cell of the launch is a parallelepiped (host-verified by
+    // bitwise edge equality, models/fused.py), so J is constant per cell and
+    // G = kappa w_a w_b adj(J) adj(J)^T / det J is formed once per thread and
+    // layer; per point only the weight w_q remains (same operator, same maths).
+    T Gc[6] = {0, 0, 0, 0, 0, 0};
+    const T kwyz = A.kappa * s_qw[NQ + a] * s_qw[NQ + b];
     {
-      const T t = s_qw[a], uu = s_qw[b];
       const T* X0 = sX;
       const T* X1 = sX + NV;
       const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
-      const int v10 = v00 + (TZ + 1) * 3, v11 = v10 + 3;
+      const int v10 = v00 + (TZ + 1) * 3;
+      if constexpr (AFF) {
+        T E[3], F[3], G[3];
 #pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const T X000 = X0[v00 + d], X001 = X0[v01 + d], X010 = X0[v10 + d], X011 = X0[v11 + d];
-        const T X100 = X1[v00 + d], X101 = X1[v01 + d], X110 = X1[v10 + d], X111 = X1[v11 + d];
-        Js[d] = (1 - t) * ((1 - uu) * (X100 - X000) + uu * (X101 - X001)) +
-                t * ((1 - uu) * (X110 - X010) + uu * (X111 - X011));
-        Jt0[d] = (1 - uu) * (X010 - X000) + uu * (X011 - X001);
-        Jt1[d] = (1 - uu) * (X110 - X100) + uu * (X111 - X101) - Jt0[d];
-        Ju0[d] = (1 - t) * (X001 - X000) + t * (X011 - X010);
-        Ju1[d] = (1 - t) * (X101 - X100) + t * (X111 - X110) - Ju0[d];
+        for (int d = 0; d < 3; ++d) {
+          const T X000 = X0[v00 + d];
+          E[d] = X1[v00 + d] - X000;
+          F[d] = X0[v10 + d] - X000;
+          G[d] = X0[v01 + d] - X000;
+        }
+        const T J00 = E[0], J10 = E[1], J20 = E[2];
+        const T J01 = F[0], J11 = F[1], J21 = F[2];
+        const T J02 = G[0], J12 = G[1], J22 = G[2];
+        const T K00 = J11 * J22 - J12 * J21, K01 = J02 * J21 - J01 * J22, K02 = J01 * J12 - J02 * J11;
+        const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
+        const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
+        const T det = J00 * K00 + J01 * K10 + J02 * K20;
+        const T sc = kwyz * fast_rcp(det);
+        Gc[0] = sc * (K00 * K00 + K01 * K01 + K02 * K02);
+        Gc[1] = sc * (K00 * K10 + K01 * K11 + K02 * K12);
+        Gc[2] = sc * (K00 * K20 + K01 * K21 + K02 * K22);
+        Gc[3] = sc * (K10 * K10 + K11 * K11 + K12 * K12);
+        Gc[4] = sc * (K10 * K20 + K11 * K21 + K12 * K22);
+        Gc[5] = sc * (K20 * K20 + K21 * K21 + K22 * K22);
+      } else {
+        const T t = s_qw[a], uu = s_qw[b];
+        const int v11 = v10 + 3;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const T X000 = X0[v00 + d], X001 = X0[v01 + d], X010 = X0[v10 + d], X011 = X0[v11 + d];
+          const T X100 = X1[v00 + d], X101 = X1[v01 + d], X110 = X1[v10 + d], X111 = X1[v11 + d];
+          Js[d] = (1 - t) * ((1 - uu) * (X100 - X000) + uu * (X101 - X001)) +
+                  t * ((1 - uu) * (X110 - X010) + uu * (X111 - X011));
+          Jt0[d] = (1 - uu) * (X010 - X000) + uu * (X011 - X001);
+          Jt1[d] = (1 - uu) * (X110 - X100) + uu * (X111 - X101) - Jt0[d];
+          Ju0[d] = (1 - t) * (X001 - X000) + t * (X011 - X010);
+          Ju1[d] = (1 - t) * (X101 - X100) + t * (X111 - X110) - Ju0[d];
+        }
       }
     }
-    const T kwyz = A.kappa * s_qw[NQ + a] * s_qw[NQ + b];
 
     // ------------------------------------------------ F = kappa G grad
     T Fx[NQ];
     using V = typename VecOf<T>::type;
     constexpr int VW = VecOf<T>::W;
     V vy, vz;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const T s = s_qw[q];
-      const T J00 = Js[0], J10 = Js[1], J20 = Js[2];
-      const T J01 = Jt0[0] + s * Jt1[0], J11 = Jt0[1] + s * Jt1[1], J21 = Jt0[2] + s * Jt1[2];
-      const T J02 = Ju0[0] + s * Ju1[0], J12 = Ju0[1] + s * Ju1[1], J22 = Ju0[2] + s * Ju1[2];
-      const T K00 = J11 * J22 - J12 * J21, K01 = J02 * J21 - J01 * J22, K02 = J01 * J12 - J02 * J11;
-      const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
-      const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
-      const T det = J00 * K00 + J01 * K10 + J02 * K20;
-      const T sc = kwyz * s_qw[NQ + q] * fast_rcp(det);
-      const T h0 = K00 * gx[q] + K10 * gy[q] + K20 * gz[q];
-      const T h1 = K01 * gx[q] + K11 * gy[q] + K21 * gz[q];
-      const T h2 = K02 * gx[q] + K12 * gy[q] + K22 * gz[q];
-      T fx = sc * (K00 * h0 + K01 * h1 + K02 * h2);
-      T fy = sc * (K10 * h0 + K11 * h1 + K12 * h2);
-      T fz = sc * (K20 * h0 + K21 * h1 + K22 * h2);
+    auto emit = [&](int q, T fx, T fy, T fz) {
       BDX_PIN3(fx, fy, fz);
       Fx[q] = fx;
       vy[q % VW] = fy;
@@ -417,6 +434,33 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
           *reinterpret_cast<V*>(w1ab + (q / VW) * VW) = vy;
           *reinterpret_cast<V*>(w3ab + (q / VW) * VW) = vz;
         }
+      }
+    };
+    if constexpr (AFF) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const T w = s_qw[NQ + q];
+        const T t0 = w * gx[q], t1 = w * gy[q], t2 = w * gz[q];
+        emit(q, Gc[0] * t0 + Gc[1] * t1 + Gc[2] * t2, Gc[1] * t0 + Gc[3] * t1 + Gc[4] * t2,
+             Gc[2] * t0 + Gc[4] * t1 + Gc[5] * t2);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const T s = s_qw[q];
+        const T J00 = Js[0], J10 = Js[1], J20 = Js[2];
+        const T J01 = Jt0[0] + s * Jt1[0], J11 = Jt0[1] + s * Jt1[1], J21 = Jt0[2] + s * Jt1[2];
+        const T J02 = Ju0[0] + s * Ju1[0], J12 = Ju0[1] + s * Ju1[1], J22 = Ju0[2] + s * Ju1[2];
+        const T K00 = J11 * J22 - J12 * J21, K01 = J02 * J21 - J01 * J22, K02 = J01 * J12 - J02 * J11;
+        const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
+        const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
+        const T det = J00 * K00 + J01 * K10 + J02 * K20;
+        const T sc = kwyz * s_qw[NQ + q] * fast_rcp(det);
+        const T h0 = K00 * gx[q] + K10 * gy[q] + K20 * gz[q];
+        const T h1 = K01 * gx[q] + K11 * gy[q] + K21 * gz[q];
+        const T h2 = K02 * gx[q] + K12 * gy[q] + K22 * gz[q];
+        emit(q, sc * (K00 * h0 + K01 * h1 + K02 * h2), sc * (K10 * h0 + K11 * h1 + K12 * h2),
+             sc * (K20 * h0 + K21 * h1 + K22 * h2));
       }
     }
     __syncthreads();
@@ -460,7 +504,8 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
 #pragma unroll
       for (int i = 0; i < ND; ++i) ye[i] = sx[i];
     } else {
-      __syncthreads();
+      // (no barrier: the transposed-gradient stage read only this lane's own
+      // w2 row; the S8 write into w1 below is ordered by the next barrier)
       if (lane_on) strow<ND>(w2ab, sx);
       __syncthreads();
       if (lane_on && a < ND) {
@@ -605,12 +650,15 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
 // descriptor (fem/mesh.py LocalLattice.as_int64) and launch one workgroup per
 // (y, z) tile.
 template <typename T, int ND, int NQ, int MODE>
-int launch_fused2(const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
+int launch_fused2(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
   using TF = TileFor<NQ>;
   using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
   const int nblk = a.nty * a.ntz;
   if (nblk <= 0) return 0;
-  lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE><<<nblk, S::threads, 0, st>>>(a, tb);
+  if (affine)
+    lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
+  else
+    lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 0><<<nblk, S::threads, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -652,7 +700,8 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
 
 #define BDX_FUSED2_TU(T, SUF, PP)                                                   \
   extern "C" int bdx_fused2_apply_##SUF##_p##PP(                                   \
-      int mode, const int64_t* latd, int nq, const double* wts, const double* qpts, \
+      int mode, int affine_ok, const int64_t* latd, int nq, const double* wts,     \
+      const double* qpts,                                                          \
       const T* u, const T* pold, T* pnew, T* y, T* yb, T* zb, T* cb, const T* xv,  \
       const T* tabs, double kappa, const double* scal, double* partials,           \
       int beta_num, int beta_den, int nty, int ntz, hipStream_t st) {              \
@@ -679,10 +728,10 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
       tb.wts[q] = q < nq ? static_cast<T>(wts[q]) : T(0);                          \
     }                                                                              \
     if (nq == PP + 1)                                                              \
-      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 1, kFusedCG>(a, tb, st) \
-                              : launch_fused2<T, PP + 1, PP + 1, kFusedAction>(a, tb, st); \
+      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 1, kFusedCG>(affine_ok, a, tb, st) \
+                              : launch_fused2<T, PP + 1, PP + 1, kFusedAction>(affine_ok, a, tb, st); \
     if (nq == PP + 2)                                                              \
-      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 2, kFusedCG>(a, tb, st) \
-                              : launch_fused2<T, PP + 1, PP + 2, kFusedAction>(a, tb, st); \
+      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 2, kFusedCG>(affine_ok, a, tb, st) \
+                              : launch_fused2<T, PP + 1, PP + 2, kFusedAction>(affine_ok, a, tb, st); \
     return static_cast<int>(hipErrorInvalidValue);                                 \
   }

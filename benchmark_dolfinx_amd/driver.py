@@ -35,12 +35,15 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
     if pb.platform == "cpu":
         return MatFreeLaplacianCPU(pb)
     if kernel == "auto":
-        kernel = "fused2" if geometry in ("auto", "otf") else "fused"
+        kernel = "fused2" if geometry in ("auto", "otf", "otf-general") else "fused"
     if kernel == "fused2":
         from .models.fused import FusedLaplacianGPU, fused_supported
-        if fused_supported(pb, 2) and geometry in ("auto", "otf"):
-            return FusedLaplacianGPU(pb, geometry="otf", version=2)
+        if fused_supported(pb, 2) and geometry in ("auto", "otf", "otf-general"):
+            return FusedLaplacianGPU(pb, geometry="otf", version=2,
+                                     affine=geometry != "otf-general")
         kernel = "fused"
+    if geometry == "otf-general":
+        geometry = "otf"
     if kernel == "fused":
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb):

@@ -39,12 +39,17 @@ class FusedLaplacianGPU:
     """version=1: lap_fused.h (OTF or stored G); version=2: lap_fused2.h
     (OTF only, precomputed per-thread addressing)."""
 
-    def __init__(self, pb, geometry: str = "otf", version: int = 1):
+    def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True):
         if geometry not in ("otf", "stored"):
             raise ValueError(f"unknown geometry mode {geometry}")
         if version == 2 and geometry != "otf":
             raise ValueError("fused2 supports on-the-fly geometry only")
         self.version = version
+        # fused2: constant-Jacobian kernel instance when every local cell is a
+        # parallelepiped (bitwise edge check on the host); else the trilinear one
+        self.affine = bool(affine and pb.all_affine)
+        if version == 2:
+            geometry = "otf-affine" if self.affine else "otf-general"
         self.name = "fused" if version == 1 else "fused2"
         self.pb = pb
         self.geometry = geometry
@@ -91,7 +96,7 @@ class FusedLaplacianGPU:
     def _launch(self, mode, u, pold, pnew, y, scal=None, beta_num=-1, beta_den=-1):
         pb, t = self.pb, self.t
         if self.version == 2:
-            _check(self._apply2(mode, ptr(pb.latd), t.nq, ptr(t.wts), ptr(t.qpts), ptr(u),
+            _check(self._apply2(mode, int(self.affine), ptr(pb.latd), t.nq, ptr(t.wts), ptr(t.qpts), ptr(u),
                                 ptr(pold), ptr(pnew), ptr(y), ptr(self.yb), ptr(self.zb),
                                 ptr(self.cb), ptr(pb.xv), ptr(self.tabs), pb.kappa, ptr(scal),
                                 ptr(self.partials), beta_num, beta_den, self.nty, self.ntz,

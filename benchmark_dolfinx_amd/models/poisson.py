@@ -36,6 +36,26 @@ def _np_dtype(dtype):
     return np.float64 if dtype == torch.float64 else np.float32
 
 
+def cells_all_parallelepipeds(X: np.ndarray) -> bool:
+    """True iff every cell of the vertex lattice X (nx+1, ny+1, nz+1, 3) has
+    bitwise-equal parallel edges (constant Jacobian).  Evaluated in the
+    kernel's precision (X's dtype), so the kernel's affine path sees exactly
+    the edge vectors checked here."""
+    if X.shape[0] < 2 or X.shape[1] < 2 or X.shape[2] < 2:
+        return True
+    for ax in range(3):
+        E = np.diff(X, axis=ax)
+        others = [d for d in range(3) if d != ax]
+        for d in others:
+            sl_a = [slice(None)] * 4
+            sl_b = [slice(None)] * 4
+            sl_a[d] = slice(0, -1)
+            sl_b[d] = slice(1, None)
+            if not np.array_equal(E[tuple(sl_a)], E[tuple(sl_b)]):
+                return False
+    return True
+
+
 class PoissonProblem:
     def __init__(self, comm: Comm, ncells, degree: int, qmode: int = 1,
                  use_gauss: bool = False, dtype=torch.float64, platform: str = "gpu",
@@ -70,6 +90,7 @@ class PoissonProblem:
         self.halo = HaloExchange(self.lat, comm, dtype, self.device, self.kernels)
         # kept alive for ctypes calls (never pass temporaries to ptr())
         self.latd = self.lat.as_int64()
+        self.all_affine = cells_all_parallelepipeds(self.xv_host)
 
     # --------------------------------------------------------------- vectors
     @property

@@ -40,7 +40,7 @@ def declare(lib) -> None:
         for P in range(1, 8):
             name = f"bdx_fused2_apply_{suf}_p{P}"
             if hasattr(lib, name):
-                _d(lib, name, [i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f64,
+                _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f64,
                                vp, vp, i32, i32, i32, i32, vp])
         _d(lib, f"bdx_fused_finalize_{suf}", [vp, vp, vp, vp, vp, i32, i32, i32, i32, vp])
         _d(lib, f"bdx_fused_tables_{suf}", [i32, i32, vp, vp, vp])

@@ -38,12 +38,13 @@ def _tol(dt):
     return 1e-12 if dt == torch.float64 else 3e-5
 
 
-VARIANTS = [("otf", 1), ("stored", 1), ("otf", 2)]
+# (geometry, kernel version, affine fast path allowed)
+VARIANTS = [("otf", 1, True), ("stored", 1, True), ("otf", 2, True), ("otf", 2, False)]
 
 
-@pytest.mark.parametrize("geometry,version", VARIANTS)
+@pytest.mark.parametrize("geometry,version,affine", VARIANTS)
 @pytest.mark.parametrize("nc,P,qm,g,pert,dt", CASES)
-def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry, version):
+def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry, version, affine):
     gpu = PoissonProblem(Comm(), nc, P, qm, g, dt, "gpu", pert)
     cpu = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "cpu", pert)
     rng = np.random.default_rng(3)
@@ -51,7 +52,7 @@ def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry, version):
     yc = cpu.new_vector()
     MatFreeLaplacianCPU(cpu).apply(u64, yc)
     yg = torch.full(gpu.lat.shape, float("nan"), dtype=dt, device=gpu.device)
-    FusedLaplacianGPU(gpu, geometry, version).apply(u64.to(gpu.device, dt), yg)
+    FusedLaplacianGPU(gpu, geometry, version, affine).apply(u64.to(gpu.device, dt), yg)
     yg = yg.double().cpu()
     o = cpu.owned
     assert torch.isfinite(o(yg)).all()
@@ -59,13 +60,15 @@ def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry, version):
     assert err <= _tol(dt) * 50 * max(1.0, yc.abs().max().item()), err
 
 
-@pytest.mark.parametrize("geometry,version", VARIANTS)
-def test_fused_cg_matches_host_cg(geometry, version):
+@pytest.mark.parametrize("geometry,version,affine", VARIANTS)
+@pytest.mark.parametrize("pert", [0.0, 0.1])
+def test_fused_cg_matches_host_cg(geometry, version, affine, pert):
     nc = (5, 7, 11)
-    gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", 0.1)
-    cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", 0.1)
+    gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", pert)
+    cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", pert)
     xg = gpu.new_vector()
-    DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, geometry, version), xg, gpu.assemble_rhs(), 30)
+    DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, geometry, version, affine), xg,
+                        gpu.assemble_rhs(), 30)
     xc = cpu.new_vector()
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 30)
     rel = (cpu.owned(xg.cpu()) - cpu.owned(xc)).abs().max().item() / xc.abs().max().item()

@@ -126,3 +126,19 @@ def test_perturbation_partition_invariant(R):
     dx = full - base
     assert np.all(dx[..., 1:] == 0) and np.abs(dx[..., 0]).max() <= 0.2 / nc[0]
     assert np.abs(dx[..., 0]).max() > 0
+
+
+def test_parallelepiped_detection():
+    from benchmark_dolfinx_amd.models.poisson import cells_all_parallelepipeds
+    lat = make_local_lattice(0, 1, (4, 5, 3), 2)
+    X = vertex_coordinates(lat, 0.0)
+    assert cells_all_parallelepipeds(X)
+    # a global affine map keeps every cell a parallelepiped (exact in binary
+    # for these dyadic coefficients)
+    A = np.array([[1.0, 0.5, 0.0], [0.0, 1.0, 0.25], [0.0, 0.0, 2.0]])
+    Xa = (X * 8).round() / 8 @ A.T
+    assert cells_all_parallelepipeds(Xa)
+    assert not cells_all_parallelepipeds(vertex_coordinates(lat, 0.1))
+    Xb = X.copy()
+    Xb[2, 2, 1, 1] += 1e-9
+    assert not cells_all_parallelepipeds(Xb)
