@@ -22,7 +22,111 @@ int pack_tables(const double* phi0, const double* dphi1, T* out) {
 }
 
 
+// CG update of the fused2 path: alpha = s[rn] / s[pap];
+//   r -= alpha (y + interface partials);  partial r.r
+// The tile-interface partials (YB/ZB/CB) are folded here on the fly instead of
+// by a separate finalize pass over y (same sum as fused_finalize_kernel).
+// x is not touched: its update x += alpha p is lagged into the next fused2
+// launch (staging reads p there anyway) and flushed by bdx_xflush at the end.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cg_update_iface_kernel(int64_t L1, int64_t ld, int64_t o0, int64_t o1, int64_t o2,
+                           int64_t Lz, T* __restrict__ r, const T* __restrict__ y,
+                           const T* __restrict__ yb, const T* __restrict__ zb,
+                           const T* __restrict__ cb, int nty, int ntz, int sy, int sz,
+                           const double* __restrict__ scal, int rn_slot, int pap_slot,
+                           double* __restrict__ partials) {
+  __shared__ double lds[16];
+  const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nrows = o0 * o1;
+  const float inv_sz = 1.0f / static_cast<float>(sz);
+  double acc = 0.0;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + wid; row < nrows;
+       row += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t i = row / o1, j = row - i * o1;
+    const int64_t base = (i * L1 + j) * ld;
+    const int tyy = static_cast<int>(j / sy);
+    const int yrow = (j % sy == 0 && tyy >= 1 && tyy < nty) ? tyy - 1 : -1;
+    const T* __restrict__ ybr = yb + (i * (nty - 1) + (yrow < 0 ? 0 : yrow)) * Lz;
+    const T* __restrict__ zbr = zb + (i * L1 + j) * (ntz - 1);
+    const T* __restrict__ cbr = cb + (i * (nty - 1) + (yrow < 0 ? 0 : yrow)) * (ntz - 1);
+    for (int k = lane; k < o2; k += 64) {
+      T v = y[base + k];
+      if (yrow >= 0) v += ybr[k];
+      int zq = static_cast<int>(static_cast<float>(k) * inv_sz);
+      if (zq * sz > k) --zq;
+      if ((zq + 1) * sz <= k) ++zq;
+      if (zq * sz == k && zq >= 1 && zq < ntz) {
+        v += zbr[zq - 1];
+        if (yrow >= 0) v += cbr[zq - 1];
+      }
+      const T rn = r[base + k] - alpha * v;
+      r[base + k] = rn;
+      acc += static_cast<double>(rn) * static_cast<double>(rn);
+    }
+  }
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+// x += (s[num] / s[den]) p over the owned rows (flush of the lagged x update).
+template <typename T>
+__global__ void __launch_bounds__(256)
+    xflush_kernel(int64_t L1, int64_t ld, int64_t o0, int64_t o1, int64_t o2, T* __restrict__ x,
+                  const T* __restrict__ p, const double* __restrict__ scal, int num, int den) {
+  const T alpha = static_cast<T>(scal[num] / scal[den]);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nrows = o0 * o1;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + wid; row < nrows;
+       row += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t i = row / o1, j = row - i * o1;
+    const int64_t base = (i * L1 + j) * ld;
+    for (int64_t k = lane; k < o2; k += 64) x[base + k] += alpha * p[base + k];
+  }
+}
+
+__global__ void reduce_partials_fixed(const double* __restrict__ partials, int n,
+                                      double* __restrict__ out, int slot) {
+  __shared__ double lds[16];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partials[i];
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) out[slot] = t;
+}
+
+static int rows_grid(int64_t nrows) {
+  const int64_t want = (nrows + 3) / 4;
+  return static_cast<int>(want < 2048 ? (want > 0 ? want : 1) : 2048);
+}
+
 extern "C" {
+
+#define BDX_CGI(T, SUF)                                                              \
+  int bdx_cg_update_iface_##SUF(const int64_t* latd, const int64_t* own, T* r,      \
+                                const T* y, const T* yb, const T* zb, const T* cb,  \
+                                int nty, int ntz, int sy, int sz, double* scal,     \
+                                int rn_slot, int pap_slot, int out_slot,            \
+                                double* partials, hipStream_t st) {                 \
+    const BdxLattice lat = BdxLattice::from(latd);                                  \
+    const int g = rows_grid(own[0] * own[1]);                                       \
+    cg_update_iface_kernel<T><<<g, 256, 0, st>>>(lat.L[1], lat.ld, own[0], own[1],  \
+                                                 own[2], lat.L[2], r, y, yb, zb, cb, \
+                                                 nty, ntz, sy, sz, scal, rn_slot,   \
+                                                 pap_slot, partials);               \
+    reduce_partials_fixed<<<1, 256, 0, st>>>(partials, g, scal, out_slot);          \
+    return static_cast<int>(hipGetLastError());                                     \
+  }                                                                                 \
+  int bdx_xflush_##SUF(const int64_t* latd, const int64_t* own, T* x, const T* p,   \
+                       const double* scal, int num, int den, hipStream_t st) {      \
+    const BdxLattice lat = BdxLattice::from(latd);                                  \
+    xflush_kernel<T><<<rows_grid(own[0] * own[1]), 256, 0, st>>>(                   \
+        lat.L[1], lat.ld, own[0], own[1], own[2], x, p, scal, num, den);            \
+    return static_cast<int>(hipGetLastError());                                     \
+  }
+BDX_CGI(double, f64)
+BDX_CGI(float, f32)
+#undef BDX_CGI
 
 // Tile shape (cells in y, z) used by the fused kernel for a given nq.
 int bdx_fused_tile(int nq, int* ty, int* tz) {
@@ -41,14 +145,14 @@ int bdx_fused_tile(int nq, int* ty, int* tz) {
 #define BDX_FIN(T, SUF)                                                          \
   int bdx_fused_finalize_##SUF(const int64_t* latd, T* y, const T* yb, const T* zb, \
                                const T* cb, int nty, int ntz, int sy, int sz,      \
-                               hipStream_t st) {                                   \
+                               int ghost_only, hipStream_t st) {                   \
     const BdxLattice lat = BdxLattice::from(latd);                                 \
     const int64_t n = lat.L[0] * (nty - 1) * lat.L[2] + lat.L[0] * lat.L[1] * (ntz - 1); \
     if (n <= 0) return 0;                                                          \
     int64_t g = (n + 255) / 256;                                                   \
     if (g > 8192) g = 8192;                                                        \
     fused_finalize_kernel<T><<<static_cast<unsigned>(g), 256, 0, st>>>(            \
-        lat, y, yb, zb, cb, nty, ntz, sy, sz);                                     \
+        lat, y, yb, zb, cb, nty, ntz, sy, sz, ghost_only);                         \
     return static_cast<int>(hipGetLastError());                                    \
   }
 

@@ -696,11 +696,14 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
 // Fold the interface partials into y (all local dofs incl. ghost planes).
 // Index space: [YB rows: Lx * (nty-1) * Lz] ++ [ZB columns not on a YB row:
 // Lx * Ly * (ntz-1)].  The two dof sets are disjoint, so no races.
+// ghost_only: fold only dofs on this rank's ghost planes (the CG path folds
+// the owned dofs inside the CG update, fused_common.hip; the ghost planes must
+// be complete before the reverse halo exchange packs them).
 template <typename T>
 __global__ void __launch_bounds__(256)
     fused_finalize_kernel(BdxLattice lat, T* __restrict__ y, const T* __restrict__ yb,
                           const T* __restrict__ zb, const T* __restrict__ cb, int nty,
-                          int ntz, int sy, int sz) {
+                          int ntz, int sy, int sz, int ghost_only) {
   const int64_t Lx = lat.L[0], Ly = lat.L[1], Lz = lat.L[2];
   const int64_t n1 = Lx * (nty - 1) * Lz;
   const int64_t n2 = Lx * Ly * (ntz - 1);
@@ -711,6 +714,7 @@ __global__ void __launch_bounds__(256)
       const int64_t r = t / Lz;
       const int64_t tym1 = r % (nty - 1), x = r / (nty - 1);
       const int64_t yy = (tym1 + 1) * sy;
+      if (ghost_only && lat.is_owned(x, yy, z)) continue;
       T add = yb[t];
       const int64_t tzz = z / sz;
       if (z % sz == 0 && tzz >= 1 && tzz < ntz) {
@@ -726,6 +730,7 @@ __global__ void __launch_bounds__(256)
       const int64_t tyy = yy / sy;
       if (yy % sy == 0 && tyy >= 1 && tyy < nty) continue;  // handled by the YB pass
       const int64_t z = (tzm1 + 1) * sz;
+      if (ghost_only && lat.is_owned(x, yy, z)) continue;
       y[lat.idx(x, yy, z)] += zb[s];
     }
   }

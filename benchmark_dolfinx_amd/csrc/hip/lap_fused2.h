@@ -25,6 +25,7 @@ struct Fused2Args {
   const T* __restrict__ u;     // action: input; CG: r
   const T* __restrict__ pold;  // CG: previous p
   T* __restrict__ pnew;        // CG: new p (tile-owned dofs)
+  T* __restrict__ x;           // CG: iterate, lagged update x += alpha_prev p_old
   T* __restrict__ y;
   T* __restrict__ yb;
   T* __restrict__ zb;
@@ -44,6 +45,7 @@ struct Fused2Args {
   int bcy_lo, bcy_hi, bcz_lo, bcz_hi;
   int nty, ntz;
   int beta_num, beta_den;        // CG: beta = scal[num] / scal[den]; num < 0 -> 0
+  int xa_num, xa_den;            // CG: alpha_prev = scal[num] / scal[den]; num < 0 -> no x update
   T kappa;
 };
 
@@ -108,9 +110,11 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   T* w2c = s_w2 + c * NQ2 * XP;
   T* w3c = s_w3 + c * NQ2 * XP;
 
-  T beta = T(0);
+  T beta = T(0), xalpha = T(0);
+  const bool xupd = MODE == kFusedCG && A.xa_num >= 0;
   if constexpr (MODE == kFusedCG) {
     if (A.beta_num >= 0) beta = static_cast<T>(A.scal[A.beta_num] / A.scal[A.beta_den]);
+    if (xupd) xalpha = static_cast<T>(A.scal[A.xa_num] / A.scal[A.xa_den]);
   }
   double pap = 0.0;
 
@@ -130,7 +134,12 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
                    int goff) -> T {
     T v;
     if constexpr (MODE == kFusedCG) {
-      v = ul[goff] + beta * A.pold[(ul - A.u) + goff];
+      const T po = A.pold[(ul - A.u) + goff];
+      v = ul[goff] + beta * po;
+      if (xupd && (f & kOwnT)) {
+        T* __restrict__ xl = A.x + (ul - A.u);
+        xl[goff] += xalpha * po;
+      }
     } else {
       v = ul[goff];
     }
@@ -262,15 +271,19 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
 
     // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
     const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
-    T pf_r[NPF], pf_p[NPF];
+    T pf_r[NPF], pf_p[NPF], pf_x[NPF];
     T pf_v[NPV];
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
       pf_r[k] = T(0);
       pf_p[k] = T(0);
+      pf_x[k] = T(0);
       if (!last && (st_meta[k] & kValid)) {
         pf_r[k] = A.u[lnext + st_goff[k]];
-        if constexpr (MODE == kFusedCG) pf_p[k] = A.pold[lnext + st_goff[k]];
+        if constexpr (MODE == kFusedCG) {
+          pf_p[k] = A.pold[lnext + st_goff[k]];
+          if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = A.x[lnext + st_goff[k]];
+        }
       }
     }
 #pragma unroll
@@ -611,7 +624,10 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
               val = pf_r[k];
             }
             if constexpr (MODE == kFusedCG) {
-              if (m & kOwnT) pnl[st_goff[k]] = val;
+              if (m & kOwnT) {
+                pnl[st_goff[k]] = val;
+                if (xupd) A.x[lnext + st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
+              }
             }
             if ((m & kBcYZ) || gxx == A.bcx_hi) {
               if (m & kOwnT) {
@@ -702,14 +718,16 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
   extern "C" int bdx_fused2_apply_##SUF##_p##PP(                                   \
       int mode, int affine_ok, const int64_t* latd, int nq, const double* wts,     \
       const double* qpts,                                                          \
-      const T* u, const T* pold, T* pnew, T* y, T* yb, T* zb, T* cb, const T* xv,  \
-      const T* tabs, double kappa, const double* scal, double* partials,           \
-      int beta_num, int beta_den, int nty, int ntz, hipStream_t st) {              \
+      const T* u, const T* pold, T* pnew, T* x, T* y, T* yb, T* zb, T* cb,         \
+      const T* xv, const T* tabs, double kappa, const double* scal,                \
+      double* partials, int beta_num, int beta_den, int xa_num, int xa_den,        \
+      int nty, int ntz, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));       \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \
+    a.x = x;                                                                       \
     a.y = y;                                                                       \
     a.yb = yb;                                                                     \
     a.zb = zb;                                                                     \
@@ -719,6 +737,8 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
     a.partials = partials;                                                         \
     a.beta_num = beta_num;                                                         \
     a.beta_den = beta_den;                                                         \
+    a.xa_num = xa_num;                                                             \
+    a.xa_den = xa_den;                                                             \
     a.kappa = static_cast<T>(kappa);                                               \
     if (!tabs) return static_cast<int>(hipErrorInvalidValue);                      \
     FusedTables<T> tb;                                                             \

@@ -93,24 +93,30 @@ class FusedLaplacianGPU:
         self.p_new = None
 
     # ------------------------------------------------------------ launches
-    def _launch(self, mode, u, pold, pnew, y, scal=None, beta_num=-1, beta_den=-1):
+    def _finalize(self, y, ghost_only: bool = False):
+        _check(self._final(ptr(self.pb.latd), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
+                           self.nty, self.ntz, self.sy, self.sz, int(ghost_only), _stream()),
+               "fused_finalize")
+
+    def _launch(self, mode, u, pold, pnew, y, scal=None, beta_num=-1, beta_den=-1, x=None,
+                xa_num=-1, xa_den=-1, finalize=True):
         pb, t = self.pb, self.t
         if self.version == 2:
-            _check(self._apply2(mode, int(self.affine), ptr(pb.latd), t.nq, ptr(t.wts), ptr(t.qpts), ptr(u),
-                                ptr(pold), ptr(pnew), ptr(y), ptr(self.yb), ptr(self.zb),
-                                ptr(self.cb), ptr(pb.xv), ptr(self.tabs), pb.kappa, ptr(scal),
-                                ptr(self.partials), beta_num, beta_den, self.nty, self.ntz,
+            _check(self._apply2(mode, int(self.affine), ptr(pb.latd), t.nq, ptr(t.wts),
+                                ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(x), ptr(y),
+                                ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(pb.xv),
+                                ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials),
+                                beta_num, beta_den, xa_num, xa_den, self.nty, self.ntz,
                                 _stream()), "fused2_apply")
-            _check(self._final(ptr(pb.latd), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
-                               self.nty, self.ntz, self.sy, self.sz, _stream()), "fused_finalize")
-            return
-        _check(self._apply(self.geom_code, mode, ptr(pb.latd), t.nq, ptr(t.phi0), ptr(t.dphi1),
-                           ptr(t.wts), ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(y),
-                           ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(self.G), ptr(pb.xv),
-                           ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials), beta_num, beta_den,
-                           self.nty, self.ntz, _stream()), "fused_apply")
-        _check(self._final(ptr(pb.latd), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
-                           self.nty, self.ntz, self.sy, self.sz, _stream()), "fused_finalize")
+        else:
+            _check(self._apply(self.geom_code, mode, ptr(pb.latd), t.nq, ptr(t.phi0),
+                               ptr(t.dphi1), ptr(t.wts), ptr(t.qpts), ptr(u), ptr(pold),
+                               ptr(pnew), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
+                               ptr(self.G), ptr(pb.xv), ptr(self.tabs), pb.kappa, ptr(scal),
+                               ptr(self.partials), beta_num, beta_den, self.nty, self.ntz,
+                               _stream()), "fused_apply")
+        if finalize:
+            self._finalize(y)
 
     def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
         """y = A u (action mode)."""
@@ -131,8 +137,12 @@ class FusedLaplacianGPU:
             self.p_new = self.pb.new_vector()
         else:
             self.p_old.zero_()
+        self.x_lag = False
+        self._own = np.array(self.pb.lat.owned_hi, dtype=np.int64)
 
     def cg_iterate(self, cg, n):
+        if self.version == 2:
+            return self._cg_iterate2(cg, n)
         k, r, y, x, scal = cg.k, cg.r, cg.y, cg.x, cg.scal
         halo = self.pb.halo
         for _ in range(n):
@@ -149,3 +159,48 @@ class FusedLaplacianGPU:
             cg._allreduce(nxt)
             self.p_old, self.p_new = self.p_new, self.p_old
             cg.it += 1
+
+    def _cg_iterate2(self, cg, n):
+        """fused2 CG iteration: x += alpha_prev p_old rides in the fused
+        kernel's staging (lagged one iteration, flushed at the end); the tile
+        interface partials are folded inside the r update (no finalize pass
+        over y; with several ranks only the ghost planes are finalized, before
+        the reverse halo packs them)."""
+        r, y, x, scal = cg.r, cg.y, cg.x, cg.scal
+        pb = self.pb
+        halo = pb.halo
+        multi = halo.active
+        upd = getattr(self.lib, f"bdx_cg_update_iface_{pb.suf}")
+        for _ in range(n):
+            cur = cg.RR0 if cg.it % 2 == 0 else cg.RR1
+            nxt = cg.RR1 if cg.it % 2 == 0 else cg.RR0
+            halo.forward(r)
+            bnum, bden = (cur, nxt) if cg.it > 0 else (-1, -1)
+            xnum, xden = (nxt, cg.PAP) if self.x_lag else (-1, -1)
+            self._launch(1, r, self.p_old, self.p_new, y, scal, bnum, bden, x, xnum, xden,
+                         finalize=False)
+            if multi:
+                self._finalize(y, ghost_only=True)
+                halo.reverse(y)
+            _check(self.lib.bdx_reduce_partials(ptr(self.partials), self.nblocks, ptr(scal),
+                                                cg.PAP, _stream()), "reduce_partials")
+            cg._allreduce(cg.PAP)
+            _check(upd(ptr(pb.latd), ptr(self._own), ptr(r), ptr(y), ptr(self.yb),
+                       ptr(self.zb), ptr(self.cb), self.nty, self.ntz, self.sy, self.sz,
+                       ptr(scal), cur, cg.PAP, nxt, ptr(cg.partials), _stream()),
+                   "cg_update_iface")
+            cg._allreduce(nxt)
+            self.p_old, self.p_new = self.p_new, self.p_old
+            self.x_lag = True
+            cg.it += 1
+        self.flush_x(cg)
+
+    def flush_x(self, cg):
+        """Apply the pending x += alpha_last p_last of the lagged update."""
+        if not self.x_lag:
+            return
+        last = cg.RR0 if (cg.it - 1) % 2 == 0 else cg.RR1
+        _check(getattr(self.lib, f"bdx_xflush_{self.pb.suf}")(
+            ptr(self.pb.latd), ptr(self._own), ptr(cg.x), ptr(self.p_old), ptr(cg.scal), last,
+            cg.PAP, _stream()), "xflush")
+        self.x_lag = False
