@@ -1,5 +1,6 @@
-// Fused-kernel helpers: tile query and the interface-partials finalize pass.
-#include "lap_fused.h"
+// Fused-kernel helpers: tile query, table packing, the interface-partials
+// finalize pass and the fused2/3 CG update.
+#include "lap_fused3.h"
 
 // Packed 1D tables of the fused kernel (layout: FusedShape::OFF_*), written
 // to host memory `out` (which the caller uploads).  Returns the count.
@@ -182,5 +183,22 @@ BDX_FIN(float, f32)
   }
 BDX_TABS(double, f64)
 BDX_TABS(float, f32)
+
+#define BDX_TABS3(T, SUF)                                                          \
+  int bdx_fused3_tables_##SUF(int nd, int nq, const double* phi0, const double* Dd, \
+                              T* out) {                                            \
+    switch (nd * 16 + nq) {                                                        \
+      case 2 * 16 + 3: return pack_tables3<T, 2, 3>(phi0, Dd, out);                \
+      case 3 * 16 + 4: return pack_tables3<T, 3, 4>(phi0, Dd, out);                \
+      case 4 * 16 + 5: return pack_tables3<T, 4, 5>(phi0, Dd, out);                \
+      case 5 * 16 + 6: return pack_tables3<T, 5, 6>(phi0, Dd, out);                \
+      case 6 * 16 + 7: return pack_tables3<T, 6, 7>(phi0, Dd, out);                \
+      case 7 * 16 + 8: return pack_tables3<T, 7, 8>(phi0, Dd, out);                \
+      case 8 * 16 + 9: return pack_tables3<T, 8, 9>(phi0, Dd, out);                \
+    }                                                                              \
+    return -1;                                                                     \
+  }
+BDX_TABS3(double, f64)
+BDX_TABS3(float, f32)
 
 }  // extern "C"

@@ -1,84 +1,35 @@
-// Fused structured operator kernel, v2 ("fused2"): the same x-march /
-// (y, z)-tile / atomic-free design as lap_fused.h (and the same operator as
-// the reference's stiffness_operator_gpu + geometry_computation_gpu,
-// src/laplacian_gpu.hpp:91-426, src/geometry_gpu.hpp:26-132), re-engineered
-// for instruction economy after rocprofv3 showed v1 spending ~45 % of its
-// VALU issue on index arithmetic and SGPR spill traffic:
+// Fused structured operator kernel, v3 ("fused3"): fused2's x-march,
+// (y, z) tiles, precomputed addressing, interface buffers and CG fusion, with
+// a re-designed contraction core (qmode=1 / Gauss, i.e. phi0 != I):
 //
-// * All per-element addressing is precomputed once per thread before the
-//   march: the input-staging elements, the output elements (their <= 4 LDS
-//   sources in the element-vector scratch, the destination class and a
-//   32-bit offset), and the vertex elements.  Per layer only 64-bit uniform
-//   base pointers advance (SGPRs), so the march body carries no 64-bit index
-//   math and no lattice struct.
-// * Dirichlet tests are per-thread bits for y/z (layer invariant) plus one
-//   compare against the local index of the global x boundary plane.
-// * 1/det uses the hardware reciprocal + two Newton steps.
-// * OTF geometry only (the stored-G layout stays on v1).
-//
-// Interface partials (YB/ZB/CB) and the finalize pass are those of v1.
+// * The reference gradient is taken directly from the dofs with the
+//   (nq x nd) table Dd = dphi1 phi0 (sum factorisation shares the B/Dd
+//   passes: z then y through LDS, x in registers), instead of interpolating
+//   to the quadrature points and differentiating there (reference
+//   src/laplacian_gpu.hpp:188-251).  The transposed path mirrors it:
+//   x in registers, then y and z through LDS.  Per cell layer this saves two
+//   workgroup barriers and about a quarter of the LDS traffic of fused2, and
+//   the x-direction passes are fused per quadrature point with the geometry
+//   (no gx/gy/gz/F arrays are kept live).
+// * When a tile cell's NQ^2 quadrature columns fill whole waves (NQ = 2, 4,
+//   8: Q6 qmode=1 is one cell per wave), the y/z contraction stages only
+//   exchange data inside a wave, so their barriers become wave-local syncs;
+//   only the dof staging and the gather keep workgroup barriers.
+// The math is the reference operator's (tests compare against the C++ CPU
+// operator and the numpy oracle); results differ only by rounding order.
 #pragma once
-#include "lap_fused.h"
+#include "lap_fused2.h"
 
-// Unroll factor of the LDS-fed contraction loops (rolled by default: keeps the
-// register budget of 3 waves/SIMD).  Timing-experiment switches BDX_X_* drop
-// a phase (WRONG numerics; only for attributing time on the GPU box).
-#ifndef BDX_MUNROLL
-#define BDX_MUNROLL 1
+#ifndef BDX_MUNROLL3
+#define BDX_MUNROLL3 2
 #endif
-#define BDX_PRAGMA(x) _Pragma(#x)
-#define BDX_PRAGMA_UNROLL(n) BDX_PRAGMA(unroll n)
-#ifndef BDX_X_NOSTAGE
-#define BDX_X_NOSTAGE 0
-#endif
-#ifndef BDX_X_NOOUT
-#define BDX_X_NOOUT 0
-#endif
-#ifndef BDX_X_NOFRONT
-#define BDX_X_NOFRONT 0
-#endif
-#ifndef BDX_X_NOGRAD
-#define BDX_X_NOGRAD 0
-#endif
-#ifndef BDX_X_NOTGRAD
-#define BDX_X_NOTGRAD 0
-#endif
-#ifndef BDX_X_NOBACK
-#define BDX_X_NOBACK 0
-#endif
-
-template <typename T>
-struct Fused2Args {
-  const T* __restrict__ u;     // action: input; CG: r
-  const T* __restrict__ pold;  // CG: previous p
-  T* __restrict__ pnew;        // CG: new p (tile-owned dofs)
-  T* __restrict__ x;           // CG: iterate, lagged update x += alpha_prev p_old
-  T* __restrict__ y;
-  T* __restrict__ yb;
-  T* __restrict__ zb;
-  T* __restrict__ cb;
-  const T* __restrict__ xv;
-  const double* __restrict__ scal;
-  double* __restrict__ partials;
-  int64_t ps;      // x-plane stride of the vectors (Ly * ld)
-  int64_t ybps;    // x-plane strides of the interface buffers
-  int64_t zbps;
-  int64_t cbps;
-  int64_t vps;     // x-plane stride of the vertex array ((n1+1)(n2+1)*3)
-  int ncx, n1, n2;
-  int Ly, Lz, ld;
-  int ownx, owny, ownz;          // rank-owned extents (L - gh)
-  int bcx_lo, bcx_hi;            // local index of the global boundary plane, -1 if none
-  int bcy_lo, bcy_hi, bcz_lo, bcz_hi;
-  int nty, ntz;
-  int beta_num, beta_den;        // CG: beta = scal[num] / scal[den]; num < 0 -> 0
-  int xa_num, xa_den;            // CG: alpha_prev = scal[num] / scal[den]; num < 0 -> no x update
-  T kappa;
-};
+// unroll of the per-quadrature-point x/F loop (full unroll hoists 2*ND*NQ
+// uniform table values into SGPRs, which spills beyond NQ = 5)
+template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 2; };
 
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
 __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
-    lap_fused2_kernel(Fused2Args<T> A, FusedTables<T> tb) {
+    lap_fused3_kernel(Fused2Args<T> A, FusedTables<T> tb) {
   using S = FusedShape<T, ND, NQ, TY, TZ>;
   constexpr int P = S::P, DY = S::DY, DZ = S::DZ, PL = DY * DZ;
   constexpr int DZP = S::DZP, PLP = DY * DZP;
@@ -91,27 +42,46 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   constexpr int NV = (TY + 1) * (TZ + 1) * 3;
   constexpr int NPV = (NV + NT - 1) / NT;
   constexpr int XP = S::XP, NP = S::NP;
-  constexpr int ZSLOT = S::work;                  // a zero row at the end of s_w2
-  static_assert(S::work + XP < 32768, "16-bit LDS source offsets");
+  // intra-cell stages only exchange data inside a wave when a cell's NQ^2
+  // columns tile whole waves
+  constexpr bool WAVELOCAL = (64 % NQ2 == 0) && (S::lanes % 64 == 0);
+  // LDS work buffers of the contraction core (rows of ND values, pitch NP):
+  //  block layout (cells straddle waves):
+  //   WB, WD [cells][ND][NQ]   z-front outputs, reused for the y-back C1, C3
+  //   A1, A2, A3 [cells][NQ][NQ] x-back outputs; A1 of cell c then holds its
+  //                            element vectors E[ND][ND]
+  //  wave-local layout: two regions R1, R2 [cells][NQ][NQ] updated in place
+  //   (a wave's LDS reads all issue before its later writes):
+  //   R1: WB -> A1 -> C1 -> E,  R2: WD -> A2 -> A3 -> C3
+  constexpr int RW = NQ2 * NP;                    // one cell's region
+  constexpr int NWB = S::cells * ND * NQ * NP;
+  constexpr int NWA = S::cells * RW;
+  constexpr int NPOOL = WAVELOCAL ? 2 * NWA : 3 * NWA;
+  constexpr int NBUF = WAVELOCAL ? 1 : 2 * NWB;
+  constexpr int ZSLOT = NPOOL;                    // zero row after the pool (offsets from R1/A1)
+  static_assert(ZSLOT + NP < 32768, "16-bit LDS source offsets");
+  static_assert(!IDENT, "fused3 is the phi0 != I core (qmode=1 or Gauss)");
+  constexpr int OFF_BR = 0, OFF_DR = NQ * NP, OFF_BC = 2 * NQ * NP, OFF_DC = 2 * NQ * NP + ND * XP;
+  constexpr int TAB3 = 2 * NQ * NP + 2 * ND * XP;
+  static_assert(TAB3 <= kFusedTabMax, "table too large");
   static_assert(PL < 256, "8-bit plane index");
 
-  __shared__ __attribute__((aligned(16))) T s_tab[S::TAB];
+  __shared__ __attribute__((aligned(16))) T s_tab[TAB3];
   __shared__ T s_qw[2 * NQ];
   __shared__ T s_u[2][ND * PLP];
   __shared__ T s_c[2][PL];
-  __shared__ __attribute__((aligned(16))) T s_w1[S::work];
-  __shared__ __attribute__((aligned(16))) T s_w2[S::work + XP];
-  __shared__ __attribute__((aligned(16))) T s_w3[S::work];
+  __shared__ __attribute__((aligned(16))) T s_wb[NBUF];
+  __shared__ __attribute__((aligned(16))) T s_wa[NPOOL + NP];
   __shared__ T s_X[2][2 * NV];
   __shared__ double s_red[16];
 
   const int tid = threadIdx.x;
-  for (int i = tid; i < S::TAB; i += NT) s_tab[i] = tb.tab[i];
+  for (int i = tid; i < TAB3; i += NT) s_tab[i] = tb.tab[i];
   if (tid < NQ) {
     s_qw[tid] = tb.qpts[tid];
     s_qw[NQ + tid] = tb.wts[tid];
   }
-  if (tid < XP) s_w2[ZSLOT + tid] = T(0);
+  if (tid < NP) s_wa[ZSLOT + tid] = T(0);
 
   // XCD-aware bijective remap of the block id (cdna_hip_programming.md T1).
   const int nblk = gridDim.x, ob = blockIdx.x;
@@ -133,9 +103,6 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   const bool lane_on = tid < S::lanes;
   const bool cell_on = lane_on && (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
   const int ycell = cy * P, zcell = cz * P;
-  T* w1c = s_w1 + c * NQ2 * XP;
-  T* w2c = s_w2 + c * NQ2 * XP;
-  T* w3c = s_w3 + c * NQ2 * XP;
 
   T beta = T(0), xalpha = T(0);
   const bool xupd = MODE == kFusedCG && A.xa_num >= 0;
@@ -221,7 +188,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         int ns = 0;
         for (int ccy = cyl; ccy <= cyh; ++ccy)
           for (int ccz = czl; ccz <= czh; ++ccz)
-            src[ns++] = (((ccy * TZ + ccz) * NQ + (ly - ccy * P)) * NQ + (lz - ccz * P)) * XP + pl;
+            src[ns++] = (ccy * TZ + ccz) * RW + ((ly - ccy * P) * ND + (lz - ccz * P)) * NP + pl;
         o_src[k][0] = src[0] | (src[1] << 16);
         o_src[k][1] = src[2] | (src[3] << 16);
         const int gy = y0 + ly, gz = z0 + lz;
@@ -326,80 +293,83 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     const T* __restrict__ sX = s_X[cur];
 
     const T* __restrict__ ua = su + (ycell + a) * DZP + zcell;
-    T* __restrict__ w1ab = w1c + (a * NQ + b) * XP;
-    T* __restrict__ w2ab = w2c + (a * NQ + b) * XP;
-    T* __restrict__ w3ab = w3c + (a * NQ + b) * XP;
-    const T* __restrict__ w1b = w1c + b * XP;
-    const T* __restrict__ w2b = w2c + b * XP;
-    const T* __restrict__ w1a = w1c + a * NQ * XP;
-    const T* __restrict__ w2a = w2c + a * NQ * XP;
-    const T* __restrict__ w3a = w3c + a * NQ * XP;
+    // (no __restrict__: the wave-local layout rewrites rows in place, so the
+    // compiler must keep each stage's LDS reads ahead of its writes)
+    T* const R1 = s_wa + c * RW;                         // wave-local regions of this cell
+    T* const R2 = s_wa + NWA + c * RW;
+    T* const wB = WAVELOCAL ? R1 - c * RW : s_wb;        // [cells][ND][NQ] bases
+    T* const wD = WAVELOCAL ? R2 - c * RW : s_wb + NWB;
+    T* const A1 = s_wa;                                  // [cells][NQ][NQ] bases
+    T* const A2 = s_wa + NWA;
+    T* const A3 = WAVELOCAL ? s_wa + NWA : s_wa + 2 * NWA;
+    // C-shape [cells][ND][NQ] offsets inside a wave-local region use the
+    // A-shape row formula (rows j < ND), so one offset expression serves both
+    auto offC = [&](int cc, int j, int q) {
+      return WAVELOCAL ? (cc * NQ + j) * NQ * NP + q * NP : ((cc * ND + j) * NQ + q) * NP;
+    };
+    auto offA = [&](int cc, int qy, int qz) { return ((cc * NQ + qy) * NQ + qz) * NP; };
+    // sync between intra-cell stages: wave-local when cells tile whole waves
+    auto cell_sync = [&]() {
+      if constexpr (WAVELOCAL) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
+        __syncthreads();
+      }
+    };
+    // compiler-level ordering of a wave's in-place LDS rewrite
+    auto wave_order = [&]() {
+      if constexpr (WAVELOCAL) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    };
 
-    // ------------------------------------------------ interpolate to qpts
-    T U[NQ];
-    if constexpr (BDX_X_NOFRONT) {
+    // ------------------------------------------------ front z: (B_z u, Dd_z u)
+    // lanes (c, j = a < ND, qz = b): rows over the cell's x dofs i
+    if (lane_on && a < ND) {
+      const T* __restrict__ br = s_tab + OFF_BR + b * NP;
+      const T* __restrict__ dr = s_tab + OFF_DR + b * NP;
+      T ob[ND], od[ND];
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[(i % ND) * PLP + (b % ND)] : T(0);
-    } else if constexpr (IDENT) {
+      for (int i = 0; i < ND; ++i) ob[i] = od[i] = T(0);
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[i * PLP + b] : T(0);
-    } else {
-      if (lane_on && a < ND) {
-        const T* __restrict__ ph = s_tab + S::OFF_PR + b * NP;
-        T o[ND];
+      for (int k = 0; k < ND; ++k) {
+        const T cb_ = br[k], cd_ = dr[k];
 #pragma unroll
-        for (int i = 0; i < ND; ++i) o[i] = 0;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-        for (int k = 0; k < ND; ++k) {
-          const T cc = ph[k];
-#pragma unroll
-          for (int i = 0; i < ND; ++i) o[i] += cc * ua[i * PLP + k];
+        for (int i = 0; i < ND; ++i) {
+          const T uv = ua[i * PLP + k];
+          ob[i] += cb_ * uv;
+          od[i] += cd_ * uv;
         }
-        strow<ND>(w1ab, o);
       }
-      __syncthreads();
-      const T* __restrict__ pa = s_tab + S::OFF_PR + a * NP;
-      T t2[ND];
-#pragma unroll
-      for (int i = 0; i < ND; ++i) t2[i] = 0;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-      for (int j = 0; j < ND; ++j) {
-        T row[ND];
-        ldrow<ND>(w1b + j * NQ * XP, row);
-        const T cc = pa[j];
-#pragma unroll
-        for (int i = 0; i < ND; ++i) t2[i] += cc * row[i];
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) U[q] = 0;
-#pragma unroll
-      for (int i = 0; i < ND; ++i) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) U[q] += gt[S::OFF_PC + i * XP + q] * t2[i];
-      }
+      const int o = offC(c, a, b);
+      strow<ND>(wB + o, ob);
+      strow<ND>(wD + o, od);
     }
+    cell_sync();
 
-    // ------------------------------------------------ reference gradient
-    if (lane_on) strow<NQ>(w2ab, U);
-    __syncthreads();
-    T gx[NQ], gy[NQ], gz[NQ];
+    // ------------------------------------------------ front y
+    // lanes (c, qy = a, qz = b): tBB = B_y B_z u, tDB = Dd_y B_z u, tBD = B_y Dd_z u
+    T tBB[ND], tDB[ND], tBD[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) tBB[i] = tDB[i] = tBD[i] = T(0);
     {
-      const T* __restrict__ dra = s_tab + S::OFF_DR + a * XP;
-      const T* __restrict__ drb = s_tab + S::OFF_DR + b * XP;
+      const T* __restrict__ bra = s_tab + OFF_BR + a * NP;
+      const T* __restrict__ dra = s_tab + OFF_DR + a * NP;
+BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
+      for (int j = 0; j < ND; ++j) {
+        T rb[ND], rd[ND];
+        const int o = offC(c, j, b);
+        ldrow<ND>(wB + o, rb);
+        ldrow<ND>(wD + o, rd);
+        const T cb_ = bra[j], cd_ = dra[j];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) gx[q] = gy[q] = gz[q] = BDX_X_NOGRAD ? U[q] : T(0);
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-      for (int m = 0; m < (BDX_X_NOGRAD ? 0 : NQ); ++m) {
-        T ry[NQ], rz[NQ];
-        ldrow<NQ>(w2b + m * NQ * XP, ry);
-        ldrow<NQ>(w2a + m * XP, rz);
-        const T um = w2ab[m], cy_ = dra[m], cz_ = drb[m];
-        const T* __restrict__ dc = gt + S::OFF_DC + m * XP;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          gx[q] += dc[q] * um;
-          gy[q] += cy_ * ry[q];
-          gz[q] += cz_ * rz[q];
+        for (int i = 0; i < ND; ++i) {
+          tBB[i] += cb_ * rb[i];
+          tDB[i] += cd_ * rb[i];
+          tBD[i] += cb_ * rd[i];
         }
       }
     }
@@ -458,38 +428,31 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
       }
     }
 
-    // ------------------------------------------------ F = kappa G grad
-    T Fx[NQ];
-    using V = typename VecOf<T>::type;
-    constexpr int VW = VecOf<T>::W;
-    V vy, vz;
-    auto emit = [&](int q, T fx, T fy, T fz) {
-      BDX_PIN3(fx, fy, fz);
-      Fx[q] = fx;
-      vy[q % VW] = fy;
-      vz[q % VW] = fz;
-      if (q % VW == VW - 1 || q == NQ - 1) {
-        if (q % VW != VW - 1) {
+    // ------------------------------------------------ x front + F + x back
+    // per quadrature point q along the thread's x column (uniform table rows):
+    //   g = (Dd_x tBB, B_x tDB, B_x tBD)(q),  F = kappa G g,
+    //   a1 += Dd_x^T Fx, a2 += B_x^T Fy, a3 += B_x^T Fz
+    T a1[ND], a2[ND], a3[ND];
 #pragma unroll
-          for (int e = q % VW + 1; e < VW; ++e) vy[e] = vz[e] = T(0);
-        }
-        if (lane_on) {
-          *reinterpret_cast<V*>(w1ab + (q / VW) * VW) = vy;
-          *reinterpret_cast<V*>(w3ab + (q / VW) * VW) = vz;
-        }
+    for (int i = 0; i < ND; ++i) a1[i] = a2[i] = a3[i] = T(0);
+BDX_PRAGMA_UNROLL(QUnroll3<NQ>::value)
+    for (int q = 0; q < NQ; ++q) {
+      T gxq = 0, gyq = 0, gzq = 0;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const T dq = gt[OFF_DC + i * XP + q], bq = gt[OFF_BC + i * XP + q];
+        gxq += dq * tBB[i];
+        gyq += bq * tDB[i];
+        gzq += bq * tBD[i];
       }
-    };
-    if constexpr (AFF) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
+      T fx, fy, fz;
+      if constexpr (AFF) {
         const T w = s_qw[NQ + q];
-        const T t0 = w * gx[q], t1 = w * gy[q], t2 = w * gz[q];
-        emit(q, Gc[0] * t0 + Gc[1] * t1 + Gc[2] * t2, Gc[1] * t0 + Gc[3] * t1 + Gc[4] * t2,
-             Gc[2] * t0 + Gc[4] * t1 + Gc[5] * t2);
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
+        const T t0 = w * gxq, t1 = w * gyq, t2 = w * gzq;
+        fx = Gc[0] * t0 + Gc[1] * t1 + Gc[2] * t2;
+        fy = Gc[1] * t0 + Gc[3] * t1 + Gc[4] * t2;
+        fz = Gc[2] * t0 + Gc[4] * t1 + Gc[5] * t2;
+      } else {
         const T s = s_qw[q];
         const T J00 = Js[0], J10 = Js[1], J20 = Js[2];
         const T J01 = Jt0[0] + s * Jt1[0], J11 = Jt0[1] + s * Jt1[1], J21 = Jt0[2] + s * Jt1[2];
@@ -499,90 +462,126 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
         const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
         const T det = J00 * K00 + J01 * K10 + J02 * K20;
         const T sc = kwyz * s_qw[NQ + q] * fast_rcp(det);
-        const T h0 = K00 * gx[q] + K10 * gy[q] + K20 * gz[q];
-        const T h1 = K01 * gx[q] + K11 * gy[q] + K21 * gz[q];
-        const T h2 = K02 * gx[q] + K12 * gy[q] + K22 * gz[q];
-        emit(q, sc * (K00 * h0 + K01 * h1 + K02 * h2), sc * (K10 * h0 + K11 * h1 + K12 * h2),
-             sc * (K20 * h0 + K21 * h1 + K22 * h2));
+        const T h0 = K00 * gxq + K10 * gyq + K20 * gzq;
+        const T h1 = K01 * gxq + K11 * gyq + K21 * gzq;
+        const T h2 = K02 * gxq + K12 * gyq + K22 * gzq;
+        fx = sc * (K00 * h0 + K01 * h1 + K02 * h2);
+        fy = sc * (K10 * h0 + K11 * h1 + K12 * h2);
+        fz = sc * (K20 * h0 + K21 * h1 + K22 * h2);
       }
-    }
-    __syncthreads();
-
-    // ------------------------------------------------ transposed gradient
-    T r[NQ];
-    {
-      if (lane_on) strow<NQ>(w2ab, Fx);
-      const T* __restrict__ dca = s_tab + S::OFF_DC + a * XP;
-      const T* __restrict__ dcb = s_tab + S::OFF_DC + b * XP;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) r[q] = BDX_X_NOTGRAD ? Fx[q] : T(0);
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-      for (int m = 0; m < (BDX_X_NOTGRAD ? 0 : NQ); ++m) {
-        T r1[NQ], r3[NQ];
-        ldrow<NQ>(w1b + m * NQ * XP, r1);
-        ldrow<NQ>(w3a + m * XP, r3);
-        const T fm = w2ab[m], ca = dca[m], cb_ = dcb[m];
-        const T* __restrict__ dr = gt + S::OFF_DR + m * XP;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) r[q] += dr[q] * fm + ca * r1[q] + cb_ * r3[q];
-      }
-    }
-    T sx[ND];
-    if constexpr (IDENT) {
-#pragma unroll
-      for (int i = 0; i < ND; ++i) sx[i] = r[i];
-    } else {
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
-        T acc = 0;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acc += gt[S::OFF_PC + i * XP + q] * r[q];
-        sx[i] = acc;
+        const T dq = gt[OFF_DC + i * XP + q], bq = gt[OFF_BC + i * XP + q];
+        a1[i] += dq * fx;
+        a2[i] += bq * fy;
+        a3[i] += bq * fz;
       }
     }
-
-    // ------------------------------------------------ back to the dofs
-    T ye[ND];
-    if constexpr (IDENT || BDX_X_NOBACK) {
+    if constexpr (WAVELOCAL) {
+      // R1 <- A1, R2 <- A2 (the front-y reads of this wave are already issued)
+      wave_order();
+      if (lane_on) {
+        strow<ND>(A1 + offA(c, a, b), a1);
+        strow<ND>(A2 + offA(c, a, b), a2);
+      }
+      cell_sync();
+      // back y, pass 1: C1 = B_y^T A1 + Dd_y^T A2 -> R1; then A3 -> R2
+      T c1[ND];
 #pragma unroll
-      for (int i = 0; i < ND; ++i) ye[i] = sx[i];
-    } else {
-      // (no barrier: the transposed-gradient stage read only this lane's own
-      // w2 row; the S8 write into w1 below is ordered by the next barrier)
-      if (lane_on) strow<ND>(w2ab, sx);
-      __syncthreads();
+      for (int i = 0; i < ND; ++i) c1[i] = T(0);
       if (lane_on && a < ND) {
-        const T* __restrict__ pca = s_tab + S::OFF_PC + a * XP;
-        T o[ND];
+        const T* bcj = s_tab + OFF_BC + a * XP;
+        const T* dcj = s_tab + OFF_DC + a * XP;
+BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
+        for (int qy = 0; qy < NQ; ++qy) {
+          T r1[ND], r2[ND];
+          ldrow<ND>(A1 + offA(c, qy, b), r1);
+          ldrow<ND>(A2 + offA(c, qy, b), r2);
+          const T bq = bcj[qy], dq = dcj[qy];
 #pragma unroll
-        for (int i = 0; i < ND; ++i) o[i] = 0;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-        for (int q = 0; q < NQ; ++q) {
-          T row[ND];
-          ldrow<ND>(w2b + q * NQ * XP, row);
-          const T cc = pca[q];
-#pragma unroll
-          for (int i = 0; i < ND; ++i) o[i] += cc * row[i];
+          for (int i = 0; i < ND; ++i) c1[i] += bq * r1[i] + dq * r2[i];
         }
-        strow<ND>(w1ab, o);
       }
-      __syncthreads();
+      wave_order();
+      if (lane_on && a < ND) strow<ND>(wB + offC(c, a, b), c1);
+      if (lane_on) strow<ND>(A3 + offA(c, a, b), a3);
+      cell_sync();
+      // pass 2: C3 = B_y^T A3 -> R2
+      T c3[ND];
 #pragma unroll
-      for (int i = 0; i < ND; ++i) ye[i] = 0;
-      if (a < ND && b < ND) {
-        const T* __restrict__ pcb = s_tab + S::OFF_PC + b * XP;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-        for (int q = 0; q < NQ; ++q) {
-          T row[ND];
-          ldrow<ND>(w1a + q * XP, row);
-          const T cc = pcb[q];
+      for (int i = 0; i < ND; ++i) c3[i] = T(0);
+      if (lane_on && a < ND) {
+        const T* bcj = s_tab + OFF_BC + a * XP;
+BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
+        for (int qy = 0; qy < NQ; ++qy) {
+          T r3[ND];
+          ldrow<ND>(A3 + offA(c, qy, b), r3);
+          const T bq = bcj[qy];
 #pragma unroll
-          for (int i = 0; i < ND; ++i) ye[i] += cc * row[i];
+          for (int i = 0; i < ND; ++i) c3[i] += bq * r3[i];
         }
+      }
+      wave_order();
+      if (lane_on && a < ND) strow<ND>(wD + offC(c, a, b), c3);
+      cell_sync();
+    } else {
+      if (lane_on) {
+        const int o = offA(c, a, b);
+        strow<ND>(A1 + o, a1);
+        strow<ND>(A2 + o, a2);
+        strow<ND>(A3 + o, a3);
+      }
+      cell_sync();
+      // back y: lanes (c, j = a < ND, qz = b): C1 = B_y^T A1 + Dd_y^T A2, C3 = B_y^T A3
+      // (into WB / WD: the front-y reads of this cell finished before the sync)
+      if (lane_on && a < ND) {
+        const T* bcj = s_tab + OFF_BC + a * XP;
+        const T* dcj = s_tab + OFF_DC + a * XP;
+        T c1[ND], c3[ND];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) c1[i] = c3[i] = T(0);
+BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
+        for (int qy = 0; qy < NQ; ++qy) {
+          const int o = offA(c, qy, b);
+          T r1[ND], r2[ND], r3[ND];
+          ldrow<ND>(A1 + o, r1);
+          ldrow<ND>(A2 + o, r2);
+          ldrow<ND>(A3 + o, r3);
+          const T bq = bcj[qy], dq = dcj[qy];
+#pragma unroll
+          for (int i = 0; i < ND; ++i) {
+            c1[i] += bq * r1[i] + dq * r2[i];
+            c3[i] += bq * r3[i];
+          }
+        }
+        const int o = offC(c, a, b);
+        strow<ND>(wB + o, c1);
+        strow<ND>(wD + o, c3);
+      }
+      cell_sync();
+    }
+
+    // ------------------------------------------------ back z
+    // lanes (c, j = a < ND, k = b < ND): y_e = B_z^T C1 + Dd_z^T C3
+    T ye[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) ye[i] = T(0);
+    if (lane_on && a < ND && b < ND) {
+      const T* bck = s_tab + OFF_BC + b * XP;
+      const T* dck = s_tab + OFF_DC + b * XP;
+BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
+      for (int qz = 0; qz < NQ; ++qz) {
+        const int o = offC(c, a, qz);
+        T r1[ND], r3[ND];
+        ldrow<ND>(wB + o, r1);
+        ldrow<ND>(wD + o, r3);
+        const T bq = bck[qz], dq = dck[qz];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) ye[i] += bq * r1[i] + dq * r3[i];
       }
     }
 
-    // ------------------------------------------------ element vectors -> LDS
+    // ------------------------------------------------ element vectors -> A1 of the cell
     const bool dof_lane = cell_on && a < ND && b < ND;
     if constexpr (MODE == kFusedCG) {
       if (dof_lane) {
@@ -591,15 +590,13 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
           pap += static_cast<double>(ua[i * PLP + b]) * static_cast<double>(ye[i]);
       }
     }
-    if constexpr (IDENT) {
-      __syncthreads();
-    }
+    wave_order();
     if (lane_on && a < ND && b < ND) {
       if (!dof_lane) {
 #pragma unroll
         for (int i = 0; i < ND; ++i) ye[i] = T(0);
       }
-      strow<ND>(w2ab, ye);
+      strow<ND>(A1 + c * RW + (a * ND + b) * NP, ye);
     }
     __syncthreads();
 
@@ -613,8 +610,8 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
         const int m = o_meta[k];
         if (BDX_X_NOOUT || !(m & kValid)) continue;
         const int pl = (m >> 8) & 15, rem = m >> 12;
-        T v = s_w2[o_src[k][0] & 0xffff] + s_w2[o_src[k][0] >> 16] +
-              s_w2[o_src[k][1] & 0xffff] + s_w2[o_src[k][1] >> 16];
+        T v = s_wa[o_src[k][0] & 0xffff] + s_wa[o_src[k][0] >> 16] +
+              s_wa[o_src[k][1] & 0xffff] + s_wa[o_src[k][1] >> 16];
         if (pl == 0) v += s_c[cur][rem];
         if (pl == P && !last) {
           s_c[nxt][rem] = v;
@@ -696,56 +693,20 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
 // descriptor (fem/mesh.py LocalLattice.as_int64) and launch one workgroup per
 // (y, z) tile.
 template <typename T, int ND, int NQ, int MODE>
-int launch_fused2(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
+int launch_fused3(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
   using TF = TileFor<NQ>;
   using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
   const int nblk = a.nty * a.ntz;
   if (nblk <= 0) return 0;
   if (affine)
-    lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
+    lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
   else
-    lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 0><<<nblk, S::threads, 0, st>>>(a, tb);
+    lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 0><<<nblk, S::threads, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());
 }
 
-template <typename T>
-inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int ntz) {
-  const BdxLattice L = BdxLattice::from(latd);
-  const int64_t P = L.P;
-  // 32-bit per-layer offsets: one layer of the vector must be < 2^31 elements
-  if ((P + 1) * L.L[1] * L.ld >= (int64_t(1) << 31)) return static_cast<int>(hipErrorInvalidValue);
-  a.ps = L.L[1] * L.ld;
-  a.ybps = static_cast<int64_t>(nty - 1) * L.L[2];
-  a.zbps = L.L[1] * static_cast<int64_t>(ntz - 1);
-  a.cbps = static_cast<int64_t>(nty - 1) * (ntz - 1);
-  a.vps = (L.n[1] + 1) * (L.n[2] + 1) * 3;
-  a.ncx = static_cast<int>(L.n[0]);
-  a.n1 = static_cast<int>(L.n[1]);
-  a.n2 = static_cast<int>(L.n[2]);
-  a.Ly = static_cast<int>(L.L[1]);
-  a.Lz = static_cast<int>(L.L[2]);
-  a.ld = static_cast<int>(L.ld);
-  a.ownx = static_cast<int>(L.L[0] - L.gh[0]);
-  a.owny = static_cast<int>(L.L[1] - L.gh[1]);
-  a.ownz = static_cast<int>(L.L[2] - L.gh[2]);
-  auto lo = [&](int d) { return L.g0[d] == 0 ? 0 : -1; };
-  auto hi = [&](int d) {
-    const int64_t i = L.N[d] - 1 - L.g0[d];
-    return (i >= 0 && i < L.L[d]) ? static_cast<int>(i) : -1;
-  };
-  a.bcx_lo = lo(0);
-  a.bcx_hi = hi(0);
-  a.bcy_lo = lo(1);
-  a.bcy_hi = hi(1);
-  a.bcz_lo = lo(2);
-  a.bcz_hi = hi(2);
-  a.nty = nty;
-  a.ntz = ntz;
-  return 0;
-}
-
-#define BDX_FUSED2_TU(T, SUF, PP)                                                   \
-  extern "C" int bdx_fused2_apply_##SUF##_p##PP(                                   \
+#define BDX_FUSED3_TU(T, SUF, PP)                                                   \
+  extern "C" int bdx_fused3_apply_##SUF##_p##PP(                                   \
       int mode, int affine_ok, const int64_t* latd, int nq, const double* wts,     \
       const double* qpts,                                                          \
       const T* u, const T* pold, T* pnew, T* x, T* y, T* yb, T* zb, T* cb,         \
@@ -777,11 +738,27 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
       tb.qpts[q] = q < nq ? static_cast<T>(qpts[q]) : T(0);                        \
       tb.wts[q] = q < nq ? static_cast<T>(wts[q]) : T(0);                          \
     }                                                                              \
-    if (nq == PP + 1)                                                              \
-      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 1, kFusedCG>(affine_ok, a, tb, st) \
-                              : launch_fused2<T, PP + 1, PP + 1, kFusedAction>(affine_ok, a, tb, st); \
     if (nq == PP + 2)                                                              \
-      return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 2, kFusedCG>(affine_ok, a, tb, st) \
-                              : launch_fused2<T, PP + 1, PP + 2, kFusedAction>(affine_ok, a, tb, st); \
+      return mode == kFusedCG ? launch_fused3<T, PP + 1, PP + 2, kFusedCG>(affine_ok, a, tb, st) \
+                              : launch_fused3<T, PP + 1, PP + 2, kFusedAction>(affine_ok, a, tb, st); \
     return static_cast<int>(hipErrorInvalidValue);                                 \
   }
+
+// Packed tables of the fused3 core (layout: OFF_BR/OFF_DR rows of B = phi0 and
+// Dd = dphi1 phi0 with pitch NP, OFF_BC/OFF_DC their transposes with pitch XP).
+template <typename T, int ND, int NQ>
+int pack_tables3(const double* phi0, const double* Dd, T* out) {
+  using S = FusedShape<T, ND, NQ, 1, 1>;
+  constexpr int NP = S::NP, XP = S::XP;
+  constexpr int OFF_BR = 0, OFF_DR = NQ * NP, OFF_BC = 2 * NQ * NP, OFF_DC = 2 * NQ * NP + ND * XP;
+  if (!out) return kFusedTabMax;
+  for (int i = 0; i < kFusedTabMax; ++i) out[i] = T(0);
+  for (int q = 0; q < NQ; ++q)
+    for (int i = 0; i < ND; ++i) {
+      out[OFF_BR + q * NP + i] = static_cast<T>(phi0[q * ND + i]);
+      out[OFF_DR + q * NP + i] = static_cast<T>(Dd[q * ND + i]);
+      out[OFF_BC + i * XP + q] = static_cast<T>(phi0[q * ND + i]);
+      out[OFF_DC + i * XP + q] = static_cast<T>(Dd[q * ND + i]);
+    }
+  return kFusedTabMax;
+}

@@ -35,7 +35,21 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
     if pb.platform == "cpu":
         return MatFreeLaplacianCPU(pb)
     if kernel == "auto":
-        kernel = "fused2" if geometry in ("auto", "otf", "otf-general") else "fused"
+        # measured on MI355X (profiles/): fused3 wins on parallelepiped meshes
+        # (Q3 +4 %, Q6 +12 % over fused2); on general trilinear meshes its
+        # larger register footprint spills at Q3, so fused2 takes those
+        if geometry == "stored":
+            kernel = "fused"
+        elif geometry == "otf-general" or not pb.all_affine:
+            kernel = "fused2"
+        else:
+            kernel = "fused3"
+    if kernel == "fused3":
+        from .models.fused import FusedLaplacianGPU, fused_supported
+        if fused_supported(pb, 3) and geometry in ("auto", "otf", "otf-general"):
+            return FusedLaplacianGPU(pb, geometry="otf", version=3,
+                                     affine=geometry != "otf-general")
+        kernel = "fused2"
     if kernel == "fused2":
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 2) and geometry in ("auto", "otf", "otf-general"):

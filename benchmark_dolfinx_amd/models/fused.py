@@ -31,26 +31,29 @@ def fused_supported(pb, version: int = 1) -> bool:
     if pb.platform != "gpu":
         return False
     lib = native.hip()
+    if version == 3 and pb.tables.is_identity:
+        return False  # fused3 is the phi0 != I core
     v = "" if version == 1 else str(version)
     return hasattr(lib, f"bdx_fused{v}_apply_{pb.suf}_p{pb.degree}")
 
 
 class FusedLaplacianGPU:
     """version=1: lap_fused.h (OTF or stored G); version=2: lap_fused2.h
-    (OTF only, precomputed per-thread addressing)."""
+    (OTF only, precomputed per-thread addressing); version=3: lap_fused3.h
+    (fused2 + direct-gradient contraction core, phi0 != I only)."""
 
     def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True):
         if geometry not in ("otf", "stored"):
             raise ValueError(f"unknown geometry mode {geometry}")
-        if version == 2 and geometry != "otf":
-            raise ValueError("fused2 supports on-the-fly geometry only")
+        if version >= 2 and geometry != "otf":
+            raise ValueError("fused2/3 support on-the-fly geometry only")
         self.version = version
         # fused2: constant-Jacobian kernel instance when every local cell is a
         # parallelepiped (bitwise edge check on the host); else the trilinear one
         self.affine = bool(affine and pb.all_affine)
-        if version == 2:
+        if version >= 2:
             geometry = "otf-affine" if self.affine else "otf-general"
-        self.name = "fused" if version == 1 else "fused2"
+        self.name = "fused" if version == 1 else f"fused{version}"
         self.pb = pb
         self.geometry = geometry
         self.lib = native.hip()
@@ -77,16 +80,23 @@ class FusedLaplacianGPU:
                 self.G = torch.empty(lat.ncells_local * 6 * t.nq ** 3, dtype=dt, device=dev)
                 pb.kernels.geometry(pb.xv, self.G)
         # packed 1D tables (uniform rows are read through scalar loads)
-        ftab = getattr(self.lib, f"bdx_fused_tables_{pb.suf}")
-        ntab = ftab(t.nd, t.nq, ptr(t.phi0), ptr(t.dphi1), None)
+        if version == 3:
+            self._Dd = np.ascontiguousarray(pb.tables.Dd, dtype=np.float64)
+            ftab = getattr(self.lib, f"bdx_fused3_tables_{pb.suf}")
+            second = self._Dd
+        else:
+            ftab = getattr(self.lib, f"bdx_fused_tables_{pb.suf}")
+            second = t.dphi1
+        ntab = ftab(t.nd, t.nq, ptr(t.phi0), ptr(second), None)
         if ntab <= 0:
             raise RuntimeError(f"no fused tables for nd={t.nd} nq={t.nq}")
         host = np.zeros(ntab, dtype=np.float64 if pb.dtype == torch.float64 else np.float32)
-        ftab(t.nd, t.nq, ptr(t.phi0), ptr(t.dphi1), ptr(host))
+        ftab(t.nd, t.nq, ptr(t.phi0), ptr(second), ptr(host))
         self.tabs = host  # host memory: copied into the kernel arguments
-        self._apply = getattr(self.lib, f"bdx_fused_apply_{pb.suf}_p{P}")
-        if version == 2:
-            self._apply2 = getattr(self.lib, f"bdx_fused2_apply_{pb.suf}_p{P}")
+        if version >= 2:
+            self._apply2 = getattr(self.lib, f"bdx_fused{version}_apply_{pb.suf}_p{P}")
+        else:
+            self._apply = getattr(self.lib, f"bdx_fused_apply_{pb.suf}_p{P}")
         self._final = getattr(self.lib, f"bdx_fused_finalize_{pb.suf}")
         self.geom_code = 1 if geometry == "otf" else 0
         self.p_old = None
@@ -101,7 +111,7 @@ class FusedLaplacianGPU:
     def _launch(self, mode, u, pold, pnew, y, scal=None, beta_num=-1, beta_den=-1, x=None,
                 xa_num=-1, xa_den=-1, finalize=True):
         pb, t = self.pb, self.t
-        if self.version == 2:
+        if self.version >= 2:
             _check(self._apply2(mode, int(self.affine), ptr(pb.latd), t.nq, ptr(t.wts),
                                 ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(x), ptr(y),
                                 ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(pb.xv),
@@ -141,7 +151,7 @@ class FusedLaplacianGPU:
         self._own = np.array(self.pb.lat.owned_hi, dtype=np.int64)
 
     def cg_iterate(self, cg, n):
-        if self.version == 2:
+        if self.version >= 2:
             return self._cg_iterate2(cg, n)
         k, r, y, x, scal = cg.k, cg.r, cg.y, cg.x, cg.scal
         halo = self.pb.halo

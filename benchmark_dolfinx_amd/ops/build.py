@@ -89,10 +89,15 @@ def hip_flags() -> list[str]:
 
 
 def build_hip(force: bool = False, jobs: int | None = None,
-              extra_flags: list[str] | None = None, variant: str = "") -> Path:
+              extra_flags: list[str] | None = None, variant: str = "",
+              only: list[str] | None = None) -> Path:
     """Build libbdx_hip.so (or, with `variant`, libbdx_hip_<variant>.so with
-    `extra_flags` appended: used for A/B kernel experiments on the GPU box)."""
+    `extra_flags` appended: used for A/B kernel experiments on the GPU box).
+    `only`: for a variant, the operator TUs (lap_fused*_*.hip stems) to keep;
+    every other operator TU is left out to save compile time."""
     srcs = _sources("hip", ".hip")
+    if only:
+        srcs = [p for p in srcs if not p.stem.startswith("lap_fused") or p.stem in only]
     flags = hip_flags() + list(extra_flags or [])
     out_so = HIP_SO if not variant else HERE / f"libbdx_hip_{variant}.so"
     obj_dir = OBJ_DIR if not variant else OBJ_DIR / variant
@@ -131,10 +136,13 @@ def main(argv=None) -> int:
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--variant", action="append", default=[],
                     help="NAME=FLAGS: also build libbdx_hip_NAME.so with extra hipcc flags")
+    ap.add_argument("--only", default="",
+                    help="comma-separated operator TU stems to keep in variant builds")
     a = ap.parse_args(argv)
+    only = [x for x in a.only.split(",") if x] or None
     for v in a.variant:
         name, _, fl = v.partition("=")
-        print("built", build_hip(a.force, a.jobs, fl.split(), name))
+        print("built", build_hip(a.force, a.jobs, fl.split(), name, only))
     if a.variant and not (a.host or a.hip):
         return 0
     both = not (a.host or a.hip)

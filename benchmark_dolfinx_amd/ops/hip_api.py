@@ -37,8 +37,8 @@ def declare(lib) -> None:
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                vp, vp, vp, vp, f64, vp, vp, i32, i32, i32, i32, vp])
-        for P in range(1, 8):
-            name = f"bdx_fused2_apply_{suf}_p{P}"
+        for P, v in [(P, v) for P in range(1, 8) for v in (2, 3)]:
+            name = f"bdx_fused{v}_apply_{suf}_p{P}"
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                vp, f64, vp, vp, i32, i32, i32, i32, i32, i32, vp])
@@ -47,6 +47,7 @@ def declare(lib) -> None:
                                                 vp, i32, i32, i32, vp, vp])
         _d(lib, f"bdx_xflush_{suf}", [vp, vp, vp, vp, vp, i32, i32, vp])
         _d(lib, f"bdx_fused_tables_{suf}", [i32, i32, vp, vp, vp])
+        _d(lib, f"bdx_fused3_tables_{suf}", [i32, i32, vp, vp, vp])
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
     _d(lib, "bdx_reduce_partials", [vp, i32, vp, i32, vp])
     del ft

@@ -39,13 +39,21 @@ def _tol(dt):
 
 
 # (geometry, kernel version, affine fast path allowed)
-VARIANTS = [("otf", 1, True), ("stored", 1, True), ("otf", 2, True), ("otf", 2, False)]
+VARIANTS = [("otf", 1, True), ("stored", 1, True), ("otf", 2, True), ("otf", 2, False),
+            ("otf", 3, True), ("otf", 3, False)]
+
+
+def _skip_unsupported(pb, version):
+    from benchmark_dolfinx_amd.models.fused import fused_supported
+    if not fused_supported(pb, version):
+        pytest.skip(f"fused{version} does not cover this element (phi0 == I)")
 
 
 @pytest.mark.parametrize("geometry,version,affine", VARIANTS)
 @pytest.mark.parametrize("nc,P,qm,g,pert,dt", CASES)
 def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry, version, affine):
     gpu = PoissonProblem(Comm(), nc, P, qm, g, dt, "gpu", pert)
+    _skip_unsupported(gpu, version)
     cpu = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "cpu", pert)
     rng = np.random.default_rng(3)
     u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
@@ -75,8 +83,8 @@ def test_fused_cg_matches_host_cg(geometry, version, affine, pert):
     assert rel < 1e-10, rel
 
 
-def _cg_job(comm, nc, P, nreps, geometry, version=1):
-    pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", 0.1)
+def _cg_job(comm, nc, P, nreps, geometry, version=1, pert=0.1):
+    pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", pert)
     u = pb.assemble_rhs()
     x = pb.new_vector()
     op = FusedLaplacianGPU(pb, geometry, version)
@@ -87,27 +95,44 @@ def _cg_job(comm, nc, P, nreps, geometry, version=1):
     return pb.norm(u), pb.norm(x), pb.norm(y)
 
 
-@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("pert", [0.0, 0.1])
+@pytest.mark.parametrize("version", [1, 2, 3])
 @pytest.mark.parametrize("ranks", [2, 4, 8])
-def test_fused_partition_invariance_threaded(ranks, version):
-    ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version)[0]
-    got = run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf", version)
+def test_fused_partition_invariance_threaded(ranks, version, pert):
+    ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert)[0]
+    got = run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert)
     for r in got:
         for a, b in zip(r, ref):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
 
 
-@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("version", [1, 2, 3])
 def test_fused_golden_and_mat_comp_16(version):
-    nx = compute_mesh_size(1000, 3)
-    pb = PoissonProblem(Comm(), nx, 3, 0, False, torch.float64, "gpu")
-    u = pb.assemble_rhs()
-    y = pb.new_vector()
-    FusedLaplacianGPU(pb, "otf", version).apply(u, y)
-    assert abs(pb.norm(y) - 9.912865833415553) < 1e-12
+    if version < 3:  # qmode=0 (phi0 == I) is not a fused3 element
+        nx = compute_mesh_size(1000, 3)
+        pb = PoissonProblem(Comm(), nx, 3, 0, False, torch.float64, "gpu")
+        u = pb.assemble_rhs()
+        y = pb.new_vector()
+        FusedLaplacianGPU(pb, "otf", version).apply(u, y)
+        assert abs(pb.norm(y) - 9.912865833415553) < 1e-12
     nx = compute_mesh_size(100000, 3)
     pb = PoissonProblem(Comm(), nx, 3, 1, False, torch.float64, "gpu")
     u = pb.assemble_rhs()
     y = pb.new_vector()
     FusedLaplacianGPU(pb, "otf", version).apply(u, y)
     assert abs(pb.norm(y) - 0.14150257625641838) < 1e-13
+
+
+@pytest.mark.parametrize("P,nc", [(1, (7, 9, 13)), (2, (5, 9, 9)), (4, (3, 5, 6)), (6, (3, 4, 5)),
+                                  (7, (2, 3, 4))])
+@pytest.mark.parametrize("pert", [0.0, 0.1])
+def test_fused3_cg_all_degrees(P, nc, pert):
+    """fused3 CG (incl. the wave-local nq = 4, 8 layouts) against the host CG."""
+    gpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "gpu", pert)
+    cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", pert)
+    xg = gpu.new_vector()
+    DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, "otf", 3), xg, gpu.assemble_rhs(), 12)
+    xc = cpu.new_vector()
+    cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 12)
+    rel = (cpu.owned(xg.cpu()) - cpu.owned(xc)).abs().max().item() / xc.abs().max().item()
+    assert rel < 1e-10, rel
