@@ -34,7 +34,7 @@ CONFIGS = {
 }
 
 
-def main(argv=None) -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -44,25 +44,29 @@ def main(argv=None) -> int:
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--geometry", default="auto")
     ap.add_argument("--platform", default="gpu")
-    a = ap.parse_args(argv)
+    return ap.parse_args(argv)
 
+
+def run(comm, a) -> dict | None:
+    """The timed CG benchmark on an initialised communicator; returns rank 0's
+    JSON record (None elsewhere).  Callable in-process (tests run it on
+    threaded ranks with RCCL semantics emulated)."""
     import torch
 
+    from benchmark_dolfinx_amd.driver import make_operator
     from benchmark_dolfinx_amd.fem.mesh import compute_mesh_size
     from benchmark_dolfinx_amd.models.poisson import PoissonProblem
-    from benchmark_dolfinx_amd.driver import make_operator
-    from benchmark_dolfinx_amd.parallel.comm import finalize, init_distributed
     from benchmark_dolfinx_amd.solvers.cg import DeviceCG, cg_solve
 
     degree, dpg, bits, base = CONFIGS[a.config]
     if a.dofs_per_gpu:
         dpg = a.dofs_per_gpu
-    comm = init_distributed(a.platform)
     n = comm.size
     if n != a.gpus and comm.rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {n}", file=sys.stderr)
     dtype = torch.float64 if bits == 64 else torch.float32
     nx = compute_mesh_size(dpg * n, degree)
+
     def log(msg):
         if comm.rank == 0:
             print(f"[bench {time.perf_counter() - t_setup:8.2f}s] {msg}", file=sys.stderr,
@@ -90,6 +94,8 @@ def main(argv=None) -> int:
         cg = DeviceCG(pb)
         cg.start(op, x, u)
         cg.iterate(a.warmup)
+    else:
+        cg_solve(op, pb, x, u, a.warmup, 0.0)
     sync()
     log("warmup done")
     t_setup = time.perf_counter() - t_setup
@@ -103,38 +109,48 @@ def main(argv=None) -> int:
     dt = comm.allreduce_scalar(dt, "max")
     value = pb.ndofs_global * a.steps / (1e9 * dt)
     ynorm = pb.norm(x)
-    if comm.rank == 0:
-        px, py, pz = pb.lat.pgrid
-        line = {
-            "metric": "GDOF/s matrix-free Laplacian apply, Q3@300M & Q6@500M dofs/GPU, "
-                      "1/2/4/8 MI355X",
-            "value": value,
-            "unit": "GDoF/s",
-            "n_gpus": n,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": 1e3 * dt / a.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": (value / (base * n)) if base else None,
-            "dtype": "fp64" if bits == 64 else "fp32",
-            "data": "synthetic (box mesh + f = 1000 exp(-((x-.5)^2+(y-.5)^2)/.02), "
-                    "as the reference)",
-            "config": {
-                "model": f"Q{degree} Poisson, qmode=1 GLL, matrix-free CG",
-                "global_batch": pb.ndofs_global,
-                "seq_len": degree,
-                "parallelism": f"dd{n} ({px}x{py}x{pz} box partition)",
-                "dofs_per_gpu": dpg,
-                "mesh": list(nx),
-                "kernel": getattr(op, "name", type(op).__name__),
-                "geometry": getattr(op, "geometry", "otf"),
-                "per_gpu_gdofs": value / n,
-                "y_norm": ynorm,
-                "setup_s": t_setup,
-                "hiplib": os.path.basename(os.environ.get("BDX_HIP_LIB", "") or "libbdx_hip.so"),
-            },
-        }
+    if comm.rank != 0:
+        return None
+    px, py, pz = pb.lat.pgrid
+    return {
+        "metric": "GDOF/s matrix-free Laplacian apply, Q3@300M & Q6@500M dofs/GPU, "
+                  "1/2/4/8 MI355X",
+        "value": value,
+        "unit": "GDoF/s",
+        "n_gpus": n,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * dt / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (value / (base * n)) if base else None,
+        "dtype": "fp64" if bits == 64 else "fp32",
+        "data": "synthetic (box mesh + f = 1000 exp(-((x-.5)^2+(y-.5)^2)/.02), "
+                "as the reference)",
+        "config": {
+            "model": f"Q{degree} Poisson, qmode=1 GLL, matrix-free CG",
+            "global_batch": pb.ndofs_global,
+            "seq_len": degree,
+            "parallelism": f"dd{n} ({px}x{py}x{pz} box partition)",
+            "dofs_per_gpu": dpg,
+            "mesh": list(nx),
+            "kernel": getattr(op, "name", type(op).__name__),
+            "geometry": getattr(op, "geometry", "otf"),
+            "per_gpu_gdofs": value / n,
+            "y_norm": ynorm,
+            "setup_s": t_setup,
+            "hiplib": os.path.basename(os.environ.get("BDX_HIP_LIB", "") or "libbdx_hip.so"),
+        },
+    }
+
+
+def main(argv=None) -> int:
+    a = parse_args(argv)
+    from benchmark_dolfinx_amd.parallel.comm import finalize, init_distributed
+
+    comm = init_distributed(a.platform)
+    line = run(comm, a)
+    if line is not None:
         print(json.dumps(line), flush=True)
     finalize()
     return 0

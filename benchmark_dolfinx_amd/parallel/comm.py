@@ -40,10 +40,17 @@ class Comm:
                "min": dist.ReduceOp.MIN}[op]
         return dist.all_reduce(t, op=rop, async_op=async_op)
 
-    def allreduce_scalar(self, v: float, op: str = "sum", device="cpu") -> float:
+    @property
+    def device(self) -> torch.device:
+        """Where this backend's collectives take tensors (RCCL: the GPU only)."""
+        if self.backend == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def allreduce_scalar(self, v: float, op: str = "sum") -> float:
         if self.size == 1:
             return float(v)
-        t = torch.tensor([float(v)], dtype=torch.float64, device=device)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
         self.allreduce_(t, op)
         return float(t.item())
 
@@ -94,18 +101,25 @@ class ThreadComm(Comm):
     in rank order, so results are deterministic.
     """
 
-    def __init__(self, group: ThreadGroup, rank: int):
+    def __init__(self, group: ThreadGroup, rank: int, emulate: str = "thread"):
         self.enabled = True
         self.rank = rank
         self.size = group.size
-        self.backend = "thread"
+        # emulate="nccl": reject host tensors in collectives like RCCL does, so
+        # single-GPU tests catch host-scalar collectives in GPU code paths
+        self.backend = emulate
         self.g = group
+
+    def _check_dev(self, t):
+        if self.backend == "nccl" and isinstance(t, torch.Tensor) and not t.is_cuda:
+            raise RuntimeError("RCCL collectives take device tensors only (got a host tensor)")
 
     def _sync_dev(self, t):
         if isinstance(t, torch.Tensor) and t.is_cuda:
             torch.cuda.synchronize(t.device)
 
     def allreduce_(self, t, op: str = "sum", async_op: bool = False):
+        self._check_dev(t)
         if self.size == 1:
             return _Done() if async_op else None
         self.g.slots[self.rank] = t.detach().clone()
@@ -127,6 +141,8 @@ class ThreadComm(Comm):
         return _Done() if async_op else None
 
     def alltoallv(self, out, inp, out_splits, in_splits, async_op: bool = False):
+        self._check_dev(out)
+        self._check_dev(inp)
         if self.size == 1:
             return _Done() if async_op else None
         self._sync_dev(inp)
@@ -156,7 +172,7 @@ class ThreadComm(Comm):
         return out
 
 
-def run_threaded(size: int, fn, *args, **kwargs):
+def run_threaded(size: int, fn, *args, emulate: str = "thread", **kwargs):
     """Run fn(comm, *args) on `size` in-process ranks; returns the per-rank results."""
     import threading
     group = ThreadGroup(size)
@@ -165,7 +181,9 @@ def run_threaded(size: int, fn, *args, **kwargs):
 
     def body(r):
         try:
-            results[r] = fn(ThreadComm(group, r), *args, **kwargs)
+            if torch.cuda.is_available():
+                torch.cuda.set_device(0)
+            results[r] = fn(ThreadComm(group, r, emulate), *args, **kwargs)
         except BaseException as e:  # pragma: no cover - re-raised below
             errors.append(e)
             group.barrier.abort()
