@@ -136,6 +136,8 @@ def run(comm, a) -> dict | None:
             "mesh": list(nx),
             "kernel": getattr(op, "name", type(op).__name__),
             "geometry": getattr(op, "geometry", "otf"),
+            "runtime": (f"native C++ ({op._rt.transport}, hipGraph={op._rt.graphs})"
+                        if getattr(op, "_rt", None) is not None else "python"),
             "per_gpu_gdofs": value / n,
             "y_norm": ynorm,
             "setup_s": t_setup,

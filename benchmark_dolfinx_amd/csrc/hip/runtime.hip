@@ -1,0 +1,552 @@
+// Native CG runtime: the whole timed CG loop of the fused operator in C++.
+//
+// The reference drives its CG from C++ (src/cg.hpp:89-169) over GPU-aware MPI
+// with host round trips per dot product and two halo scatters per iteration
+// (SURVEY.md quirks Q2/Q3).  This runtime owns one rank's iteration:
+//
+//   [halo fwd of r]  fused2/3(CG)  [ghost finalize + halo rev of y]
+//   reduce(p.Ap) -> all-reduce(device scalar) -> r update (+ r.r) -> all-reduce
+//
+// on one HIP stream, with every scalar device-resident, the halo as grouped
+// RCCL point-to-point sends/receives with the <= 7 (faces/edges/corner)
+// neighbours over xGMI, and the steady-state iterations (two parities: the
+// p buffers and the r.r slots ping-pong) captured once into hipGraphs and
+// replayed.  A second transport runs R ranks as threads of one process on one
+// GPU (host barriers + device copies) so the multi-rank orchestration is
+// testable on a single-GPU box; graphs are used with RCCL or a single rank.
+//
+// Python (solvers/native.py) builds the problem, runs the CG prologue
+// (r0 = b - A x0, rho0) and hands the device buffers to this runtime.
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "bdx_common.h"
+
+extern "C" {
+int bdx_box_copy_f64(int, double*, int64_t, int64_t, const int64_t*, int, int64_t, double*,
+                     hipStream_t);
+int bdx_box_copy_f32(int, float*, int64_t, int64_t, const int64_t*, int, int64_t, float*,
+                     hipStream_t);
+int bdx_reduce_partials(const double*, int, double*, int, hipStream_t);
+int bdx_fused_finalize_f64(const int64_t*, double*, const double*, const double*,
+                           const double*, int, int, int, int, int, hipStream_t);
+int bdx_fused_finalize_f32(const int64_t*, float*, const float*, const float*, const float*,
+                           int, int, int, int, int, hipStream_t);
+int bdx_cg_update_iface_f64(const int64_t*, const int64_t*, double*, const double*,
+                            const double*, const double*, const double*, int, int, int, int,
+                            double*, int, int, int, double*, hipStream_t);
+int bdx_cg_update_iface_f32(const int64_t*, const int64_t*, float*, const float*, const float*,
+                            const float*, const float*, int, int, int, int, double*, int, int,
+                            int, double*, hipStream_t);
+int bdx_xflush_f64(const int64_t*, const int64_t*, double*, const double*, const double*, int,
+                   int, hipStream_t);
+int bdx_xflush_f32(const int64_t*, const int64_t*, float*, const float*, const double*, int,
+                   int, hipStream_t);
+}
+
+// The fused2/3 operator entry points (lap_fused{2,3}_<suf>_p<P>.hip).
+#define BDX_DECL_APPLY(V, T, SUF, PP)                                                        \
+  extern "C" int bdx_fused##V##_apply_##SUF##_p##PP(                                        \
+      int, int, const int64_t*, int, const double*, const double*, const T*, const T*, T*, \
+      T*, T*, T*, T*, T*, const T*, const T*, double, const double*, double*, int, int, int, \
+      int, int, int, hipStream_t);
+#define BDX_DECL_ALL(V)                                                                    \
+  BDX_DECL_APPLY(V, double, f64, 1) BDX_DECL_APPLY(V, double, f64, 2)                      \
+  BDX_DECL_APPLY(V, double, f64, 3) BDX_DECL_APPLY(V, double, f64, 4)                      \
+  BDX_DECL_APPLY(V, double, f64, 5) BDX_DECL_APPLY(V, double, f64, 6)                      \
+  BDX_DECL_APPLY(V, double, f64, 7) BDX_DECL_APPLY(V, float, f32, 1)                       \
+  BDX_DECL_APPLY(V, float, f32, 2) BDX_DECL_APPLY(V, float, f32, 3)                        \
+  BDX_DECL_APPLY(V, float, f32, 4) BDX_DECL_APPLY(V, float, f32, 5)                        \
+  BDX_DECL_APPLY(V, float, f32, 6) BDX_DECL_APPLY(V, float, f32, 7)
+BDX_DECL_ALL(2)
+BDX_DECL_ALL(3)
+
+namespace {
+
+template <typename T>
+using ApplyFn = int (*)(int, int, const int64_t*, int, const double*, const double*, const T*,
+                        const T*, T*, T*, T*, T*, T*, T*, const T*, const T*, double,
+                        const double*, double*, int, int, int, int, int, int, hipStream_t);
+
+template <typename T>
+ApplyFn<T> apply_fn(int version, int P);
+template <>
+ApplyFn<double> apply_fn<double>(int version, int P) {
+#define BDX_CASE(V, PP) \
+  if (version == V && P == PP) return &bdx_fused##V##_apply_f64_p##PP;
+  BDX_CASE(2, 1) BDX_CASE(2, 2) BDX_CASE(2, 3) BDX_CASE(2, 4) BDX_CASE(2, 5) BDX_CASE(2, 6)
+  BDX_CASE(2, 7) BDX_CASE(3, 1) BDX_CASE(3, 2) BDX_CASE(3, 3) BDX_CASE(3, 4) BDX_CASE(3, 5)
+  BDX_CASE(3, 6) BDX_CASE(3, 7)
+#undef BDX_CASE
+  return nullptr;
+}
+template <>
+ApplyFn<float> apply_fn<float>(int version, int P) {
+#define BDX_CASE(V, PP) \
+  if (version == V && P == PP) return &bdx_fused##V##_apply_f32_p##PP;
+  BDX_CASE(2, 1) BDX_CASE(2, 2) BDX_CASE(2, 3) BDX_CASE(2, 4) BDX_CASE(2, 5) BDX_CASE(2, 6)
+  BDX_CASE(2, 7) BDX_CASE(3, 1) BDX_CASE(3, 2) BDX_CASE(3, 3) BDX_CASE(3, 4) BDX_CASE(3, 5)
+  BDX_CASE(3, 6) BDX_CASE(3, 7)
+#undef BDX_CASE
+  return nullptr;
+}
+
+// ------------------------------------------------------------------ transports
+struct Transport {
+  virtual ~Transport() = default;
+  // Grouped point-to-point exchange: rank p receives rcnt[p] elements from
+  // each peer (into rbuf + roff[p]) and sends scnt[p] elements to it.
+  virtual int exchange(const void* sbuf, const std::vector<int64_t>& scnt,
+                       const std::vector<int64_t>& soff, void* rbuf,
+                       const std::vector<int64_t>& rcnt, const std::vector<int64_t>& roff,
+                       int esize, hipStream_t st) = 0;
+  virtual int allreduce_sum(double* dev, int n, hipStream_t st) = 0;
+  virtual bool capturable() const = 0;
+};
+
+struct RcclTransport final : Transport {
+  ncclComm_t comm = nullptr;
+  int nranks = 1;
+  ~RcclTransport() override {
+    if (comm) ncclCommDestroy(comm);
+  }
+  int exchange(const void* sbuf, const std::vector<int64_t>& scnt,
+               const std::vector<int64_t>& soff, void* rbuf, const std::vector<int64_t>& rcnt,
+               const std::vector<int64_t>& roff, int esize, hipStream_t st) override {
+    const ncclDataType_t dt = esize == 8 ? ncclFloat64 : ncclFloat32;
+    if (ncclGroupStart() != ncclSuccess) return -1;
+    for (int p = 0; p < nranks; ++p) {
+      if (scnt[p] > 0 &&
+          ncclSend(static_cast<const char*>(sbuf) + soff[p] * esize, scnt[p], dt, p, comm, st) !=
+              ncclSuccess)
+        return -2;
+      if (rcnt[p] > 0 &&
+          ncclRecv(static_cast<char*>(rbuf) + roff[p] * esize, rcnt[p], dt, p, comm, st) !=
+              ncclSuccess)
+        return -3;
+    }
+    return ncclGroupEnd() == ncclSuccess ? 0 : -4;
+  }
+  int allreduce_sum(double* dev, int n, hipStream_t st) override {
+    return ncclAllReduce(dev, dev, n, ncclFloat64, ncclSum, comm, st) == ncclSuccess ? 0 : -5;
+  }
+  bool capturable() const override { return true; }
+};
+
+// R ranks = R threads of one process on one device (tests): host barriers,
+// device-to-device copies from the peers' posted buffers, fixed-order sums.
+struct ThreadGroupState {
+  std::mutex m;
+  std::condition_variable cv;
+  int size = 0, arrived = 0;
+  long generation = 0;
+  std::vector<const void*> sbuf;
+  std::vector<const std::vector<int64_t>*> soff;
+  std::vector<double*> red;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const long gen = generation;
+    if (++arrived == size) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != gen; });
+    }
+  }
+};
+std::mutex g_groups_m;
+std::map<int64_t, std::shared_ptr<ThreadGroupState>> g_groups;
+
+struct ThreadTransport final : Transport {
+  std::shared_ptr<ThreadGroupState> g;
+  int rank = 0;
+  int exchange(const void* sbuf, const std::vector<int64_t>& scnt,
+               const std::vector<int64_t>& soff, void* rbuf, const std::vector<int64_t>& rcnt,
+               const std::vector<int64_t>& roff, int esize, hipStream_t st) override {
+    (void)scnt;
+    BDX_CHECK(hipStreamSynchronize(st));
+    g->sbuf[rank] = sbuf;
+    g->soff[rank] = &soff;
+    g->barrier();
+    for (int p = 0; p < g->size; ++p) {
+      if (rcnt[p] <= 0) continue;
+      const char* src = static_cast<const char*>(g->sbuf[p]) + (*g->soff[p])[rank] * esize;
+      BDX_CHECK(hipMemcpyAsync(static_cast<char*>(rbuf) + roff[p] * esize, src, rcnt[p] * esize,
+                               hipMemcpyDeviceToDevice, st));
+    }
+    BDX_CHECK(hipStreamSynchronize(st));
+    g->barrier();
+    return 0;
+  }
+  int allreduce_sum(double* dev, int n, hipStream_t st) override {
+    BDX_CHECK(hipStreamSynchronize(st));
+    g->red[rank] = dev;
+    g->barrier();
+    std::vector<double> acc(n, 0.0), v(n);
+    for (int p = 0; p < g->size; ++p) {  // fixed rank order: deterministic
+      BDX_CHECK(hipMemcpy(v.data(), g->red[p], n * sizeof(double), hipMemcpyDeviceToHost));
+      for (int i = 0; i < n; ++i) acc[i] += v[i];
+    }
+    g->barrier();
+    BDX_CHECK(hipMemcpy(dev, acc.data(), n * sizeof(double), hipMemcpyHostToDevice));
+    g->barrier();
+    return 0;
+  }
+  bool capturable() const override { return false; }
+};
+
+// ------------------------------------------------------------------ the CG loop
+constexpr int kRR0 = 0, kRR1 = 1, kPAP = 2;
+
+struct RtConfig {
+  int64_t latd[17];
+  int64_t own[3];
+  int version, affine, P, nq, nblocks, nty, ntz, sy, sz;
+  double kappa;
+  std::vector<double> wts, qpts;
+};
+
+template <typename T>
+struct CGRuntime {
+  RtConfig cfg;
+  std::unique_ptr<Transport> tr;
+  int nranks = 1;
+  // own non-blocking stream (graph capture is not allowed on the legacy
+  // default stream torch may be using); ordered against the caller's stream
+  // `ext` with events at the start and end of every iterate()
+  hipStream_t st = nullptr, ext = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  ApplyFn<T> apply = nullptr;
+  std::vector<T> tabs;
+  T *x, *r, *pa, *pb, *y, *yb, *zb, *cb;
+  const T* xv;
+  double *scal, *partials, *upart;
+  // halo: owned lower faces <-> ghost planes (parallel/halo.py layout)
+  bool halo = false;
+  T *hbuf_a = nullptr, *hbuf_b = nullptr;
+  const int64_t *face_boxes = nullptr, *ghost_boxes = nullptr;
+  int nface_boxes = 0, nghost_boxes = 0;
+  int64_t face_total = 0, ghost_total = 0;
+  std::vector<int64_t> face_cnt, face_off, ghost_cnt, ghost_off;
+  // state
+  long it = 0;
+  bool x_lag = false;
+  bool use_graph = true, graph_ok[2] = {false, false};
+  hipGraphExec_t graph[2] = {nullptr, nullptr};
+
+  int box_copy(int mode, T* vec, const int64_t* boxes, int nb, int64_t total, T* buf) {
+    const BdxLattice L = BdxLattice::from(cfg.latd);
+    if constexpr (sizeof(T) == 8)
+      return bdx_box_copy_f64(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, st);
+    else
+      return bdx_box_copy_f32(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, st);
+  }
+  int halo_forward(T* v) {
+    BDX_CHECK(static_cast<hipError_t>(box_copy(0, v, face_boxes, nface_boxes, face_total, hbuf_a)));
+    int rc = tr->exchange(hbuf_a, face_cnt, face_off, hbuf_b, ghost_cnt, ghost_off, sizeof(T), st);
+    if (rc) return rc;
+    return box_copy(1, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_b);
+  }
+  int halo_reverse(T* v) {
+    BDX_CHECK(static_cast<hipError_t>(box_copy(0, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_a)));
+    int rc = tr->exchange(hbuf_a, ghost_cnt, ghost_off, hbuf_b, face_cnt, face_off, sizeof(T), st);
+    if (rc) return rc;
+    return box_copy(2, v, face_boxes, nface_boxes, face_total, hbuf_b);
+  }
+
+  // One CG iteration with explicit parity / flags (stream-ordered, no sync).
+  int step(long k, bool first, bool xlag) {
+    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
+    T* pold = (k % 2 == 0) ? pa : pb;
+    T* pnew = (k % 2 == 0) ? pb : pa;
+    int rc;
+    if (halo && (rc = halo_forward(r))) return rc;
+    rc = apply(1, cfg.affine, cfg.latd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold, pnew,
+               x, y, yb, zb, cb, xv, tabs.data(), cfg.kappa, scal, partials,
+               first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1, cfg.nty,
+               cfg.ntz, st);
+    if (rc) return rc;
+    if (halo) {
+      if constexpr (sizeof(T) == 8)
+        rc = bdx_fused_finalize_f64(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1, st);
+      else
+        rc = bdx_fused_finalize_f32(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1, st);
+      if (rc || (rc = halo_reverse(y))) return rc;
+    }
+    if ((rc = bdx_reduce_partials(partials, cfg.nblocks, scal, kPAP, st))) return rc;
+    if (nranks > 1 && (rc = tr->allreduce_sum(scal + kPAP, 1, st))) return rc;
+    if constexpr (sizeof(T) == 8)
+      rc = bdx_cg_update_iface_f64(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
+                                   cfg.sz, scal, cur, kPAP, nxt, upart, st);
+    else
+      rc = bdx_cg_update_iface_f32(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
+                                   cfg.sz, scal, cur, kPAP, nxt, upart, st);
+    if (rc) return rc;
+    if (nranks > 1 && (rc = tr->allreduce_sum(scal + nxt, 1, st))) return rc;
+    return 0;
+  }
+
+  // Capture the steady-state iteration of a parity (it > 0, lagged x update).
+  bool capture(int parity) {
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    const int rc = step(parity, false, true);
+    const hipError_t e = hipStreamEndCapture(st, &g);
+    if (rc || e != hipSuccess || !g) {
+      if (g) hipGraphDestroy(g);
+      (void)hipGetLastError();
+      return false;
+    }
+    const bool ok = hipGraphInstantiate(&graph[parity], g, nullptr, nullptr, 0) == hipSuccess;
+    hipGraphDestroy(g);
+    if (!ok) (void)hipGetLastError();
+    return ok;
+  }
+
+  int iterate(long n) {
+    BDX_CHECK(hipEventRecord(ev_in, ext));
+    BDX_CHECK(hipStreamWaitEvent(st, ev_in, 0));
+    int rc = iterate_on_stream(n);
+    BDX_CHECK(hipEventRecord(ev_out, st));
+    BDX_CHECK(hipStreamWaitEvent(ext, ev_out, 0));
+    return rc;
+  }
+
+  int iterate_on_stream(long n) {
+    for (long i = 0; i < n; ++i) {
+      const bool first = (it == 0);
+      const int par = static_cast<int>(it % 2);
+      if (!first && x_lag && use_graph && tr->capturable()) {
+        if (!graph_ok[par]) {
+          graph_ok[par] = capture(par);
+          if (!graph_ok[par]) use_graph = false;  // fall back to eager launches
+        }
+      }
+      if (!first && x_lag && use_graph && graph_ok[par]) {
+        BDX_CHECK(hipGraphLaunch(graph[par], st));
+      } else {
+        const int rc = step(it, first, x_lag);
+        if (rc) return rc;
+      }
+      x_lag = true;
+      ++it;
+    }
+    return flush();
+  }
+
+  int flush() {
+    if (!x_lag) return 0;
+    const int last = ((it - 1) % 2 == 0) ? kRR0 : kRR1;
+    T* plast = ((it - 1) % 2 == 0) ? pb : pa;  // p_new of the last iteration
+    x_lag = false;
+    if constexpr (sizeof(T) == 8)
+      return bdx_xflush_f64(cfg.latd, cfg.own, x, plast, scal, last, kPAP, st);
+    else
+      return bdx_xflush_f32(cfg.latd, cfg.own, x, plast, scal, last, kPAP, st);
+  }
+
+  ~CGRuntime() {
+    for (auto& g : graph)
+      if (g) hipGraphExecDestroy(g);
+    if (ev_in) hipEventDestroy(ev_in);
+    if (ev_out) hipEventDestroy(ev_out);
+    if (st) hipStreamDestroy(st);
+  }
+};
+
+struct Handle {
+  int is_f64;
+  void* rt;
+};
+
+template <typename T>
+Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, double kappa,
+               const double* wts, const double* qpts, const void* tabs, void* const* ptrs,
+               const int64_t* halo_sizes, const int64_t* face_cnt, const int64_t* ghost_cnt,
+               int transport, int nranks, int rank, const void* uid, int64_t group_id,
+               hipStream_t st) {
+  auto* rt = new CGRuntime<T>();
+  RtConfig& c = rt->cfg;
+  std::memcpy(c.latd, latd, sizeof(c.latd));
+  std::memcpy(c.own, own, sizeof(c.own));
+  // iparams: version, affine, P, nq, nblocks, nty, ntz, sy, sz, use_graph
+  c.version = iparams[0];
+  c.affine = iparams[1];
+  c.P = iparams[2];
+  c.nq = iparams[3];
+  c.nblocks = iparams[4];
+  c.nty = iparams[5];
+  c.ntz = iparams[6];
+  c.sy = iparams[7];
+  c.sz = iparams[8];
+  rt->use_graph = iparams[9] != 0;
+  c.kappa = kappa;
+  c.wts.assign(wts, wts + c.nq);
+  c.qpts.assign(qpts, qpts + c.nq);
+  rt->apply = apply_fn<T>(c.version, c.P);
+  if (!rt->apply) {
+    delete rt;
+    return nullptr;
+  }
+  const T* tb = static_cast<const T*>(tabs);
+  rt->tabs.assign(tb, tb + 384);  // kFusedTabMax (lap_fused.h)
+  int i = 0;
+  rt->x = static_cast<T*>(ptrs[i++]);
+  rt->r = static_cast<T*>(ptrs[i++]);
+  rt->pa = static_cast<T*>(ptrs[i++]);
+  rt->pb = static_cast<T*>(ptrs[i++]);
+  rt->y = static_cast<T*>(ptrs[i++]);
+  rt->yb = static_cast<T*>(ptrs[i++]);
+  rt->zb = static_cast<T*>(ptrs[i++]);
+  rt->cb = static_cast<T*>(ptrs[i++]);
+  rt->xv = static_cast<const T*>(ptrs[i++]);
+  rt->scal = static_cast<double*>(ptrs[i++]);
+  rt->partials = static_cast<double*>(ptrs[i++]);
+  rt->upart = static_cast<double*>(ptrs[i++]);
+  rt->hbuf_a = static_cast<T*>(ptrs[i++]);
+  rt->hbuf_b = static_cast<T*>(ptrs[i++]);
+  rt->face_boxes = static_cast<const int64_t*>(ptrs[i++]);
+  rt->ghost_boxes = static_cast<const int64_t*>(ptrs[i++]);
+  rt->nface_boxes = static_cast<int>(halo_sizes[0]);
+  rt->face_total = halo_sizes[1];
+  rt->nghost_boxes = static_cast<int>(halo_sizes[2]);
+  rt->ghost_total = halo_sizes[3];
+  rt->nranks = nranks;
+  rt->ext = st;
+  if (hipStreamCreateWithFlags(&rt->st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&rt->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&rt->ev_out, hipEventDisableTiming) != hipSuccess) {
+    delete rt;
+    return nullptr;
+  }
+  rt->face_cnt.assign(face_cnt, face_cnt + nranks);
+  rt->ghost_cnt.assign(ghost_cnt, ghost_cnt + nranks);
+  rt->face_off.assign(nranks, 0);
+  rt->ghost_off.assign(nranks, 0);
+  for (int p = 1; p < nranks; ++p) {
+    rt->face_off[p] = rt->face_off[p - 1] + rt->face_cnt[p - 1];
+    rt->ghost_off[p] = rt->ghost_off[p - 1] + rt->ghost_cnt[p - 1];
+  }
+  rt->halo = nranks > 1 && (rt->face_total + rt->ghost_total) > 0;
+  if (transport == 1 && nranks > 1) {  // RCCL
+    auto t = std::make_unique<RcclTransport>();
+    t->nranks = nranks;
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    if (ncclCommInitRank(&t->comm, nranks, id, rank) != ncclSuccess) {
+      delete rt;
+      return nullptr;
+    }
+    rt->tr = std::move(t);
+  } else if (transport == 2 && nranks > 1) {  // in-process threads
+    auto t = std::make_unique<ThreadTransport>();
+    {
+      std::lock_guard<std::mutex> lk(g_groups_m);
+      auto& g = g_groups[group_id];
+      if (!g) {
+        g = std::make_shared<ThreadGroupState>();
+        g->size = nranks;
+        g->sbuf.assign(nranks, nullptr);
+        g->soff.assign(nranks, nullptr);
+        g->red.assign(nranks, nullptr);
+      }
+      t->g = g;
+    }
+    t->rank = rank;
+    rt->tr = std::move(t);
+  } else {  // single rank: no communication
+    auto t = std::make_unique<RcclTransport>();
+    t->nranks = 1;
+    rt->tr = std::move(t);
+    rt->halo = false;
+  }
+  return new Handle{sizeof(T) == 8, rt};
+}
+
+}  // namespace
+
+extern "C" {
+
+int bdx_rt_nccl_unique_id(void* out128) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  std::memcpy(out128, &id, sizeof(id));
+  return static_cast<int>(sizeof(id));
+}
+
+void* bdx_rt_create(int is_f64, const int64_t* latd, const int64_t* own, const int* iparams,
+                    double kappa, const double* wts, const double* qpts, const void* tabs,
+                    void* const* ptrs, const int64_t* halo_sizes, const int64_t* face_cnt,
+                    const int64_t* ghost_cnt, int transport, int nranks, int rank,
+                    const void* uid, int64_t group_id, hipStream_t st) {
+  if (is_f64)
+    return create<double>(latd, own, iparams, kappa, wts, qpts, tabs, ptrs, halo_sizes,
+                          face_cnt, ghost_cnt, transport, nranks, rank, uid, group_id, st);
+  return create<float>(latd, own, iparams, kappa, wts, qpts, tabs, ptrs, halo_sizes, face_cnt,
+                       ghost_cnt, transport, nranks, rank, uid, group_id, st);
+}
+
+// Reset the CG state after a new prologue (p_a zeroed by the caller).
+int bdx_rt_reset(void* h) {
+  auto* H = static_cast<Handle*>(h);
+  if (H->is_f64) {
+    auto* rt = static_cast<CGRuntime<double>*>(H->rt);
+    rt->it = 0;
+    rt->x_lag = false;
+  } else {
+    auto* rt = static_cast<CGRuntime<float>*>(H->rt);
+    rt->it = 0;
+    rt->x_lag = false;
+  }
+  return 0;
+}
+
+int bdx_rt_iterate(void* h, long n) {
+  auto* H = static_cast<Handle*>(h);
+  if (H->is_f64) return static_cast<CGRuntime<double>*>(H->rt)->iterate(n);
+  return static_cast<CGRuntime<float>*>(H->rt)->iterate(n);
+}
+
+// it (iterations done) and whether steady-state graphs are in use.
+int bdx_rt_state(void* h, long* it, int* graphs) {
+  auto* H = static_cast<Handle*>(h);
+  if (H->is_f64) {
+    auto* rt = static_cast<CGRuntime<double>*>(H->rt);
+    *it = rt->it;
+    *graphs = rt->use_graph && (rt->graph_ok[0] || rt->graph_ok[1]);
+  } else {
+    auto* rt = static_cast<CGRuntime<float>*>(H->rt);
+    *it = rt->it;
+    *graphs = rt->use_graph && (rt->graph_ok[0] || rt->graph_ok[1]);
+  }
+  return 0;
+}
+
+void bdx_rt_destroy(void* h) {
+  auto* H = static_cast<Handle*>(h);
+  if (!H) return;
+  if (H->is_f64)
+    delete static_cast<CGRuntime<double>*>(H->rt);
+  else
+    delete static_cast<CGRuntime<float>*>(H->rt);
+  delete H;
+}
+
+void bdx_rt_release_group(int64_t group_id) {
+  std::lock_guard<std::mutex> lk(g_groups_m);
+  g_groups.erase(group_id);
+}
+
+}  // extern "C"

@@ -42,12 +42,17 @@ class FusedLaplacianGPU:
     (OTF only, precomputed per-thread addressing); version=3: lap_fused3.h
     (fused2 + direct-gradient contraction core, phi0 != I only)."""
 
-    def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True):
+    def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True,
+                 runtime: str = "native"):
         if geometry not in ("otf", "stored"):
             raise ValueError(f"unknown geometry mode {geometry}")
         if version >= 2 and geometry != "otf":
             raise ValueError("fused2/3 support on-the-fly geometry only")
         self.version = version
+        # CG loop driver for fused2/3: "native" = C++ runtime (solvers/native.py),
+        # "python" = the launch sequence below driven from Python
+        self.runtime = runtime if version >= 2 else "python"
+        self._rt = None
         # fused2: constant-Jacobian kernel instance when every local cell is a
         # parallelepiped (bitwise edge check on the host); else the trilinear one
         self.affine = bool(affine and pb.all_affine)
@@ -149,8 +154,24 @@ class FusedLaplacianGPU:
             self.p_old.zero_()
         self.x_lag = False
         self._own = np.array(self.pb.lat.owned_hi, dtype=np.int64)
+        if self.runtime == "native":
+            if self._rt is None or self._rt.cg is not cg:
+                from ..solvers.native import NativeCGRuntime
+                if self._rt is not None:
+                    self._rt.close()
+                try:
+                    self._rt = NativeCGRuntime(self, cg)
+                except RuntimeError as e:  # e.g. RCCL bootstrap failure: stay correct
+                    import sys
+                    print(f"[bdx] native CG runtime unavailable ({e}); using the Python "
+                          f"driver of the same kernels", file=sys.stderr)
+                    self.runtime, self._rt = "python", None
+            if self._rt is not None:
+                self._rt.reset()
 
     def cg_iterate(self, cg, n):
+        if self.version >= 2 and self._rt is not None:
+            return self._rt.iterate(n)
         if self.version >= 2:
             return self._cg_iterate2(cg, n)
         k, r, y, x, scal = cg.k, cg.r, cg.y, cg.x, cg.scal

@@ -121,8 +121,10 @@ def build_hip(force: bool = False, jobs: int | None = None,
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
     tmp = out_so.with_suffix(".so.tmp")
+    # RCCL: resolved at load time against the librccl.so.1 torch already
+    # loaded (same SONAME), so the process holds one RCCL
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={HIP_ARCH}", *map(str, objs),
-          "-o", str(tmp)])
+          "-L/opt/rocm/lib", "-lrccl", "-o", str(tmp)])
     os.replace(tmp, out_so)
     _stamp(out_so, digest)
     return out_so

@@ -49,5 +49,14 @@ def declare(lib) -> None:
         _d(lib, f"bdx_fused_tables_{suf}", [i32, i32, vp, vp, vp])
         _d(lib, f"bdx_fused3_tables_{suf}", [i32, i32, vp, vp, vp])
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
+    # native CG runtime (runtime.hip)
+    _d(lib, "bdx_rt_nccl_unique_id", [vp])
+    _d(lib, "bdx_rt_create", [i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
+                              vp, i64, vp], vp)
+    _d(lib, "bdx_rt_reset", [vp])
+    _d(lib, "bdx_rt_iterate", [vp, ctypes.c_long])
+    _d(lib, "bdx_rt_state", [vp, vp, vp])
+    _d(lib, "bdx_rt_destroy", [vp], None)
+    _d(lib, "bdx_rt_release_group", [i64], None)
     _d(lib, "bdx_reduce_partials", [vp, i32, vp, i32, vp])
     del ft

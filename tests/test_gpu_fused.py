@@ -68,14 +68,17 @@ def test_fused_action_matches_cpu(nc, P, qm, g, pert, dt, geometry, version, aff
     assert err <= _tol(dt) * 50 * max(1.0, yc.abs().max().item()), err
 
 
+@pytest.mark.parametrize("runtime", ["native", "python"])
 @pytest.mark.parametrize("geometry,version,affine", VARIANTS)
 @pytest.mark.parametrize("pert", [0.0, 0.1])
-def test_fused_cg_matches_host_cg(geometry, version, affine, pert):
+def test_fused_cg_matches_host_cg(geometry, version, affine, pert, runtime):
+    if version == 1 and runtime == "native":
+        pytest.skip("the native runtime drives fused2/3")
     nc = (5, 7, 11)
     gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", pert)
     cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", pert)
     xg = gpu.new_vector()
-    DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, geometry, version, affine), xg,
+    DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, geometry, version, affine, runtime), xg,
                         gpu.assemble_rhs(), 30)
     xc = cpu.new_vector()
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 30)
@@ -83,11 +86,11 @@ def test_fused_cg_matches_host_cg(geometry, version, affine, pert):
     assert rel < 1e-10, rel
 
 
-def _cg_job(comm, nc, P, nreps, geometry, version=1, pert=0.1):
+def _cg_job(comm, nc, P, nreps, geometry, version=1, pert=0.1, runtime="native"):
     pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", pert)
     u = pb.assemble_rhs()
     x = pb.new_vector()
-    op = FusedLaplacianGPU(pb, geometry, version)
+    op = FusedLaplacianGPU(pb, geometry, version, runtime=runtime)
     DeviceCG(pb).solve(op, x, u, nreps)
     y = pb.new_vector()
     op.apply(u, y)
@@ -95,12 +98,15 @@ def _cg_job(comm, nc, P, nreps, geometry, version=1, pert=0.1):
     return pb.norm(u), pb.norm(x), pb.norm(y)
 
 
+@pytest.mark.parametrize("runtime", ["native", "python"])
 @pytest.mark.parametrize("pert", [0.0, 0.1])
 @pytest.mark.parametrize("version", [1, 2, 3])
 @pytest.mark.parametrize("ranks", [2, 4, 8])
-def test_fused_partition_invariance_threaded(ranks, version, pert):
-    ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert)[0]
-    got = run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert)
+def test_fused_partition_invariance_threaded(ranks, version, pert, runtime):
+    if version == 1 and runtime == "native":
+        pytest.skip("the native runtime drives fused2/3")
+    ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert, runtime)[0]
+    got = run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert, runtime)
     for r in got:
         for a, b in zip(r, ref):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
