@@ -52,19 +52,38 @@ __global__ void __launch_bounds__(256)
     const T* __restrict__ ybr = yb + (i * (nty - 1) + (yrow < 0 ? 0 : yrow)) * Lz;
     const T* __restrict__ zbr = zb + (i * L1 + j) * (ntz - 1);
     const T* __restrict__ cbr = cb + (i * (nty - 1) + (yrow < 0 ? 0 : yrow)) * (ntz - 1);
-    for (int k = lane; k < o2; k += 64) {
-      T v = y[base + k];
-      if (yrow >= 0) v += ybr[k];
-      int zq = static_cast<int>(static_cast<float>(k) * inv_sz);
-      if (zq * sz > k) --zq;
-      if ((zq + 1) * sz <= k) ++zq;
-      if (zq * sz == k && zq >= 1 && zq < ntz) {
-        v += zbr[zq - 1];
-        if (yrow >= 0) v += cbr[zq - 1];
+    // 16-byte vectors along the row (rows start 128-byte aligned: the storage
+    // pitch ld is a multiple of 16 elements); per element the interface terms
+    constexpr int W = 16 / sizeof(T);
+    typedef T V __attribute__((ext_vector_type(W)));
+    for (int k0 = lane * W; k0 < o2; k0 += 64 * W) {
+      const bool full = k0 + W <= o2;
+      V vy, vr;
+      if (full) {
+        vy = *reinterpret_cast<const V*>(y + base + k0);
+        vr = *reinterpret_cast<const V*>(r + base + k0);
       }
-      const T rn = r[base + k] - alpha * v;
-      r[base + k] = rn;
-      acc += static_cast<double>(rn) * static_cast<double>(rn);
+#pragma unroll
+      for (int e = 0; e < W; ++e) {
+        const int k = k0 + e;
+        if (k >= o2) break;
+        T v = full ? vy[e] : y[base + k];
+        if (yrow >= 0) v += ybr[k];
+        int zq = static_cast<int>(static_cast<float>(k) * inv_sz);
+        if (zq * sz > k) --zq;
+        if ((zq + 1) * sz <= k) ++zq;
+        if (zq * sz == k && zq >= 1 && zq < ntz) {
+          v += zbr[zq - 1];
+          if (yrow >= 0) v += cbr[zq - 1];
+        }
+        const T rn = (full ? vr[e] : r[base + k]) - alpha * v;
+        if (full)
+          vr[e] = rn;
+        else
+          r[base + k] = rn;
+        acc += static_cast<double>(rn) * static_cast<double>(rn);
+      }
+      if (full) *reinterpret_cast<V*>(r + base + k0) = vr;
     }
   }
   const double t = block_sum(acc, lds);
@@ -148,12 +167,24 @@ int bdx_fused_tile(int nq, int* ty, int* tz) {
                                const T* cb, int nty, int ntz, int sy, int sz,      \
                                int ghost_only, hipStream_t st) {                   \
     const BdxLattice lat = BdxLattice::from(latd);                                 \
+    if (ghost_only) {                                                              \
+      const int64_t Lx = lat.L[0], Ly = lat.L[1], Lz = lat.L[2];                   \
+      const int64_t xB = lat.gh[0] ? Lx - 1 : Lx;                                  \
+      const int64_t n = (lat.gh[0] ? (nty - 1) * Lz + Ly * (ntz - 1) : 0) +        \
+                        (lat.gh[1] ? xB * (ntz - 1) : 0) + (lat.gh[2] ? xB * (nty - 1) : 0); \
+      if (n <= 0) return 0;                                                        \
+      int64_t g = (n + 255) / 256;                                                 \
+      if (g > 4096) g = 4096;                                                      \
+      fused_finalize_ghost_kernel<T><<<static_cast<unsigned>(g), 256, 0, st>>>(    \
+          lat, y, yb, zb, cb, nty, ntz, sy, sz);                                   \
+      return static_cast<int>(hipGetLastError());                                  \
+    }                                                                              \
     const int64_t n = lat.L[0] * (nty - 1) * lat.L[2] + lat.L[0] * lat.L[1] * (ntz - 1); \
     if (n <= 0) return 0;                                                          \
     int64_t g = (n + 255) / 256;                                                   \
     if (g > 8192) g = 8192;                                                        \
     fused_finalize_kernel<T><<<static_cast<unsigned>(g), 256, 0, st>>>(            \
-        lat, y, yb, zb, cb, nty, ntz, sy, sz, ghost_only);                         \
+        lat, y, yb, zb, cb, nty, ntz, sy, sz, 0);                                  \
     return static_cast<int>(hipGetLastError());                                    \
   }
 

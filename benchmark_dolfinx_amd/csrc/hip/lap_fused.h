@@ -735,3 +735,53 @@ __global__ void __launch_bounds__(256)
     }
   }
 }
+
+// Ghost-plane-only finalize (multi-rank CG path): the same sums as
+// fused_finalize_kernel, restricted to the interface entries whose dof lies on
+// one of this rank's ghost planes (x = Lx-1, y = Ly-1, z = Lz-1 when that
+// plane is a ghost plane).  Interface rows/columns are never on the y/z ghost
+// planes themselves ((nt-1)*TP < n*P), so three compact index ranges cover it:
+//   A: x = Lx-1: every YB row (with its ZB/CB crossings) and every ZB column
+//      not on a YB row;  B: y = Ly-1, ZB columns (x < Lx-1 if A ran);
+//   C: z = Lz-1, YB rows (x < Lx-1 if A ran).
+template <typename T>
+__global__ void __launch_bounds__(256)
+    fused_finalize_ghost_kernel(BdxLattice lat, T* __restrict__ y, const T* __restrict__ yb,
+                                const T* __restrict__ zb, const T* __restrict__ cb, int nty,
+                                int ntz, int sy, int sz) {
+  const int64_t Lx = lat.L[0], Ly = lat.L[1], Lz = lat.L[2];
+  const bool gx = lat.gh[0], gy = lat.gh[1], gz = lat.gh[2];
+  const int64_t xB = gx ? Lx - 1 : Lx;  // x range of parts B, C
+  const int64_t nA1 = gx ? (nty - 1) * Lz : 0, nA2 = gx ? Ly * (ntz - 1) : 0;
+  const int64_t nB = gy ? xB * (ntz - 1) : 0;
+  const int64_t nC = gz ? xB * (nty - 1) : 0;
+  const int64_t ntot = nA1 + nA2 + nB + nC;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < ntot;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    if (t < nA1) {  // YB row entry on the x ghost plane
+      const int64_t x = Lx - 1, z = t % Lz, tym1 = t / Lz;
+      const int64_t yy = (tym1 + 1) * sy;
+      T add = yb[(x * (nty - 1) + tym1) * Lz + z];
+      const int64_t tzz = z / sz;
+      if (z % sz == 0 && tzz >= 1 && tzz < ntz) {
+        add += zb[(x * Ly + yy) * (ntz - 1) + (tzz - 1)];
+        add += cb[(x * (nty - 1) + tym1) * (ntz - 1) + (tzz - 1)];
+      }
+      y[lat.idx(x, yy, z)] += add;
+    } else if (t < nA1 + nA2) {  // ZB column entry on the x ghost plane
+      const int64_t s = t - nA1, x = Lx - 1;
+      const int64_t tzm1 = s % (ntz - 1), yy = s / (ntz - 1);
+      const int64_t tyy = yy / sy;
+      if (yy % sy == 0 && tyy >= 1 && tyy < nty) continue;  // on a YB row: done above
+      y[lat.idx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
+    } else if (t < nA1 + nA2 + nB) {  // ZB column entry on the y ghost plane
+      const int64_t s = t - nA1 - nA2, yy = Ly - 1;
+      const int64_t tzm1 = s % (ntz - 1), x = s / (ntz - 1);
+      y[lat.idx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
+    } else {  // YB row entry on the z ghost plane
+      const int64_t s = t - nA1 - nA2 - nB, z = Lz - 1;
+      const int64_t tym1 = s % (nty - 1), x = s / (nty - 1);
+      y[lat.idx(x, (tym1 + 1) * sy, z)] += yb[(x * (nty - 1) + tym1) * Lz + z];
+    }
+  }
+}

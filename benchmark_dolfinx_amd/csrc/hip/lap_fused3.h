@@ -25,6 +25,25 @@
 #endif
 // unroll of the per-quadrature-point x/F loop (full unroll hoists 2*ND*NQ
 // uniform table values into SGPRs, which spills beyond NQ = 5)
+// timing experiments (WRONG numerics): drop one stage / the intra-cell barriers
+#ifndef BDX_X3_NOFZ
+#define BDX_X3_NOFZ 0
+#endif
+#ifndef BDX_X3_NOFY
+#define BDX_X3_NOFY 0
+#endif
+#ifndef BDX_X3_NOXF
+#define BDX_X3_NOXF 0
+#endif
+#ifndef BDX_X3_NOBY
+#define BDX_X3_NOBY 0
+#endif
+#ifndef BDX_X3_NOBZ
+#define BDX_X3_NOBZ 0
+#endif
+#ifndef BDX_X3_NOSYNC
+#define BDX_X3_NOSYNC 0
+#endif
 template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 2; };
 
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
@@ -314,7 +333,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      } else {
+      } else if constexpr (!BDX_X3_NOSYNC) {
         __syncthreads();
       }
     };
@@ -328,7 +347,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
 
     // ------------------------------------------------ front z: (B_z u, Dd_z u)
     // lanes (c, j = a < ND, qz = b): rows over the cell's x dofs i
-    if (lane_on && a < ND) {
+    if (!BDX_X3_NOFZ && lane_on && a < ND) {
       const T* __restrict__ br = s_tab + OFF_BR + b * NP;
       const T* __restrict__ dr = s_tab + OFF_DR + b * NP;
       T ob[ND], od[ND];
@@ -359,7 +378,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
       const T* __restrict__ bra = s_tab + OFF_BR + a * NP;
       const T* __restrict__ dra = s_tab + OFF_DR + a * NP;
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
-      for (int j = 0; j < ND; ++j) {
+      for (int j = 0; j < (BDX_X3_NOFY ? 0 : ND); ++j) {
         T rb[ND], rd[ND];
         const int o = offC(c, j, b);
         ldrow<ND>(wB + o, rb);
@@ -436,7 +455,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
 #pragma unroll
     for (int i = 0; i < ND; ++i) a1[i] = a2[i] = a3[i] = T(0);
 BDX_PRAGMA_UNROLL(QUnroll3<NQ>::value)
-    for (int q = 0; q < NQ; ++q) {
+    for (int q = 0; q < (BDX_X3_NOXF ? 1 : NQ); ++q) {
       T gxq = 0, gyq = 0, gzq = 0;
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
@@ -541,7 +560,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
 #pragma unroll
         for (int i = 0; i < ND; ++i) c1[i] = c3[i] = T(0);
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
-        for (int qy = 0; qy < NQ; ++qy) {
+        for (int qy = 0; qy < (BDX_X3_NOBY ? 0 : NQ); ++qy) {
           const int o = offA(c, qy, b);
           T r1[ND], r2[ND], r3[ND];
           ldrow<ND>(A1 + o, r1);
@@ -570,7 +589,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
       const T* bck = s_tab + OFF_BC + b * XP;
       const T* dck = s_tab + OFF_DC + b * XP;
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
-      for (int qz = 0; qz < NQ; ++qz) {
+      for (int qz = 0; qz < (BDX_X3_NOBZ ? 0 : NQ); ++qz) {
         const int o = offC(c, a, qz);
         T r1[ND], r3[ND];
         ldrow<ND>(wB + o, r1);
