@@ -110,8 +110,36 @@ class PoissonProblem:
             self.comm.allreduce_(s.view(1) if s.dim() == 0 else s)
         return float(s.item())
 
-    def norm(self, v: torch.Tensor) -> float:
-        return math.sqrt(max(self.inner(v, v), 0.0))
+    def norm(self, v: torch.Tensor, kind: str = "l2") -> float:
+        """l2 or linf norm over the owned dofs (reference la::norm,
+        src/vector.hpp:196-218; linf here is max |v|, not the reference's
+        |max v| (quirk Q7))."""
+        if kind == "l2":
+            return math.sqrt(max(self.inner(v, v), 0.0))
+        if kind != "linf":
+            raise ValueError(f"unknown norm {kind}")
+        m = torch.max(torch.abs(self.owned(v))).double().reshape(1)
+        if self.comm.size > 1:
+            m = m.to(self.comm.device)
+            self.comm.allreduce_(m, "max")
+        return float(m.item())
+
+    # BLAS-1 over the owned dofs (reference src/vector.hpp:228-292: axpy,
+    # scale, copy, pointwise_mult, set_value); vectors keep the padded layout
+    def axpy(self, out: torch.Tensor, alpha: float, x: torch.Tensor, y: torch.Tensor) -> None:
+        self.owned(out).copy_(alpha * self.owned(x) + self.owned(y))
+
+    def scale(self, v: torch.Tensor, alpha: float) -> None:
+        self.owned(v).mul_(alpha)
+
+    def copy(self, dst: torch.Tensor, src: torch.Tensor) -> None:
+        self.owned(dst).copy_(self.owned(src))
+
+    def pointwise_mult(self, out: torch.Tensor, x: torch.Tensor, y: torch.Tensor) -> None:
+        self.owned(out).copy_(self.owned(x) * self.owned(y))
+
+    def set_value(self, v: torch.Tensor, value: float) -> None:
+        v.fill_(value)  # owned + ghost, like the reference
 
     def bc_mask(self) -> torch.Tensor:
         m = np.zeros(self.lat.shape, dtype=bool)

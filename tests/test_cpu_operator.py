@@ -157,3 +157,27 @@ def test_partition_invariance_threaded(R):
         assert abs(res[1] - ref[1]) < 1e-12 * ref[1]
         assert res[2] < 1e-12 * ref[1]
         assert abs(res[3] - ref[3]) < 1e-10 * ref[3]
+
+
+@pytest.mark.parametrize("R", [1, 3])
+def test_norms_and_blas1(R):
+    def body(comm):
+        pb = _problem((4, 3, 5), 2, 1, comm=comm)
+        u = pb.assemble_rhs()
+        v = pb.new_vector()
+        pb.copy(v, u)
+        pb.scale(v, -2.0)
+        w = pb.new_vector()
+        pb.axpy(w, 0.5, v, u)          # 0.5 * (-2u) + u = 0
+        z = pb.new_vector()
+        pb.pointwise_mult(z, u, u)
+        return (pb.norm(u), pb.norm(v, "linf"), pb.norm(w), pb.inner(z, pb.new_vector() + 1.0),
+                pb.norm(u) ** 2)
+
+    res = run_threaded(R, body)
+    ref = body(Comm())
+    for r in res:
+        assert abs(r[0] - ref[0]) < 1e-14 * ref[0]
+        assert abs(r[1] - ref[1]) < 1e-14 * ref[1]   # linf = max |v| (not |max v|)
+        assert r[2] < 1e-15
+        assert abs(r[3] - r[4]) < 1e-12 * r[4]          # sum(u*u) == ||u||^2
