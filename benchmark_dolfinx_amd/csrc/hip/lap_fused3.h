@@ -64,20 +64,26 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   // intra-cell stages only exchange data inside a wave when a cell's NQ^2
   // columns tile whole waves
   constexpr bool WAVELOCAL = (64 % NQ2 == 0) && (S::lanes % 64 == 0);
-  // LDS work buffers of the contraction core (rows of ND values, pitch NP):
-  //  block layout (cells straddle waves):
-  //   WB, WD [cells][ND][NQ]   z-front outputs, reused for the y-back C1, C3
-  //   A1, A2, A3 [cells][NQ][NQ] x-back outputs; A1 of cell c then holds its
-  //                            element vectors E[ND][ND]
-  //  wave-local layout: two regions R1, R2 [cells][NQ][NQ] updated in place
-  //   (a wave's LDS reads all issue before its later writes):
-  //   R1: WB -> A1 -> C1 -> E,  R2: WD -> A2 -> A3 -> C3
-  constexpr int RW = NQ2 * NP;                    // one cell's region
-  constexpr int NWB = S::cells * ND * NQ * NP;
-  constexpr int NWA = S::cells * RW;
-  constexpr int NPOOL = WAVELOCAL ? 2 * NWA : 3 * NWA;
-  constexpr int NBUF = WAVELOCAL ? 1 : 2 * NWB;
-  constexpr int ZSLOT = NPOOL;                    // zero row after the pool (offsets from R1/A1)
+  // LDS work buffers of the contraction core: NBUFS buffers W[k][cell][i1][i2]
+  // of rows of ND values.  Padded for conflict-free 16-byte LDS access
+  // (scripts/lds_bank_sim.py; measured: unpadded Q6 lost 56 % of its LDS
+  // cycles to bank conflicts): the row pitch RP, the i1 pitch P1 and the cell
+  // pitch PC are odd numbers of 16-byte slots, so the rows one ds_read_b128 /
+  // ds_write_b128 touches (varying i2, or varying i1) start on distinct banks.
+  //  block layout (cells straddle waves), 3 buffers:
+  //    W0: B_z u -> A1 -> C1      W1: Dd_z u -> A2 -> C3      W2: A3 -> E
+  //  wave-local layout, 2 buffers updated in place (a wave's LDS reads all
+  //  issue before its later writes):
+  //    W0: B_z u -> A1 -> C1 -> E  W1: Dd_z u -> A2 -> A3 -> C3
+  constexpr int VW = VecOf<T>::W;
+  constexpr int odd_slots_rp = (NP / VW) % 2 ? NP / VW : NP / VW + 1;
+  constexpr int RP = odd_slots_rp * VW;
+  constexpr int P1 = ((NQ * RP / VW) % 2 ? NQ * RP / VW : NQ * RP / VW + 1) * VW;
+  constexpr int PC = ((NQ * P1 / VW) % 2 ? NQ * P1 / VW : NQ * P1 / VW + 1) * VW;
+  constexpr int NBUFS = WAVELOCAL ? 2 : 3;
+  constexpr int NWBUF = S::cells * PC;            // one buffer
+  constexpr int EBUF = WAVELOCAL ? 0 : 2;         // buffer holding the element vectors
+  constexpr int ZSLOT = NBUFS * NWBUF;            // zero row after the pool
   static_assert(ZSLOT + NP < 32768, "16-bit LDS source offsets");
   static_assert(!IDENT, "fused3 is the phi0 != I core (qmode=1 or Gauss)");
   constexpr int OFF_BR = 0, OFF_DR = NQ * NP, OFF_BC = 2 * NQ * NP, OFF_DC = 2 * NQ * NP + ND * XP;
@@ -89,8 +95,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   __shared__ T s_qw[2 * NQ];
   __shared__ T s_u[2][ND * PLP];
   __shared__ T s_c[2][PL];
-  __shared__ __attribute__((aligned(16))) T s_wb[NBUF];
-  __shared__ __attribute__((aligned(16))) T s_wa[NPOOL + NP];
+  __shared__ __attribute__((aligned(16))) T s_wa[NBUFS * NWBUF + RP];
   __shared__ T s_X[2][2 * NV];
   __shared__ double s_red[16];
 
@@ -100,7 +105,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     s_qw[tid] = tb.qpts[tid];
     s_qw[NQ + tid] = tb.wts[tid];
   }
-  if (tid < NP) s_wa[ZSLOT + tid] = T(0);
+  if (tid < RP) s_wa[ZSLOT + tid] = T(0);
 
   // XCD-aware bijective remap of the block id (cdna_hip_programming.md T1).
   const int nblk = gridDim.x, ob = blockIdx.x;
@@ -207,7 +212,8 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         int ns = 0;
         for (int ccy = cyl; ccy <= cyh; ++ccy)
           for (int ccz = czl; ccz <= czh; ++ccz)
-            src[ns++] = (ccy * TZ + ccz) * RW + ((ly - ccy * P) * ND + (lz - ccz * P)) * NP + pl;
+            src[ns++] = EBUF * NWBUF + (ccy * TZ + ccz) * PC + (ly - ccy * P) * P1 +
+                        (lz - ccz * P) * RP + pl;
         o_src[k][0] = src[0] | (src[1] << 16);
         o_src[k][1] = src[2] | (src[3] << 16);
         const int gy = y0 + ly, gz = z0 + lz;
@@ -314,19 +320,10 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     const T* __restrict__ ua = su + (ycell + a) * DZP + zcell;
     // (no __restrict__: the wave-local layout rewrites rows in place, so the
     // compiler must keep each stage's LDS reads ahead of its writes)
-    T* const R1 = s_wa + c * RW;                         // wave-local regions of this cell
-    T* const R2 = s_wa + NWA + c * RW;
-    T* const wB = WAVELOCAL ? R1 - c * RW : s_wb;        // [cells][ND][NQ] bases
-    T* const wD = WAVELOCAL ? R2 - c * RW : s_wb + NWB;
-    T* const A1 = s_wa;                                  // [cells][NQ][NQ] bases
-    T* const A2 = s_wa + NWA;
-    T* const A3 = WAVELOCAL ? s_wa + NWA : s_wa + 2 * NWA;
-    // C-shape [cells][ND][NQ] offsets inside a wave-local region use the
-    // A-shape row formula (rows j < ND), so one offset expression serves both
-    auto offC = [&](int cc, int j, int q) {
-      return WAVELOCAL ? (cc * NQ + j) * NQ * NP + q * NP : ((cc * ND + j) * NQ + q) * NP;
-    };
-    auto offA = [&](int cc, int qy, int qz) { return ((cc * NQ + qy) * NQ + qz) * NP; };
+    T* const W0 = s_wa;
+    T* const W1 = s_wa + NWBUF;
+    T* const W2 = s_wa + 2 * NWBUF;  // block layout only
+    auto offA = [&](int cc, int i1, int i2) { return cc * PC + i1 * P1 + i2 * RP; };
     // sync between intra-cell stages: wave-local when cells tile whole waves
     auto cell_sync = [&]() {
       if constexpr (WAVELOCAL) {
@@ -363,9 +360,9 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
           od[i] += cd_ * uv;
         }
       }
-      const int o = offC(c, a, b);
-      strow<ND>(wB + o, ob);
-      strow<ND>(wD + o, od);
+      const int o = offA(c, a, b);
+      strow<ND>(W0 + o, ob);
+      strow<ND>(W1 + o, od);
     }
     cell_sync();
 
@@ -380,9 +377,9 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
       for (int j = 0; j < (BDX_X3_NOFY ? 0 : ND); ++j) {
         T rb[ND], rd[ND];
-        const int o = offC(c, j, b);
-        ldrow<ND>(wB + o, rb);
-        ldrow<ND>(wD + o, rd);
+        const int o = offA(c, j, b);
+        ldrow<ND>(W0 + o, rb);
+        ldrow<ND>(W1 + o, rd);
         const T cb_ = bra[j], cd_ = dra[j];
 #pragma unroll
         for (int i = 0; i < ND; ++i) {
@@ -497,14 +494,14 @@ BDX_PRAGMA_UNROLL(QUnroll3<NQ>::value)
       }
     }
     if constexpr (WAVELOCAL) {
-      // R1 <- A1, R2 <- A2 (the front-y reads of this wave are already issued)
+      // W0 <- A1, W1 <- A2 (the front-y reads of this wave are already issued)
       wave_order();
       if (lane_on) {
-        strow<ND>(A1 + offA(c, a, b), a1);
-        strow<ND>(A2 + offA(c, a, b), a2);
+        strow<ND>(W0 + offA(c, a, b), a1);
+        strow<ND>(W1 + offA(c, a, b), a2);
       }
       cell_sync();
-      // back y, pass 1: C1 = B_y^T A1 + Dd_y^T A2 -> R1; then A3 -> R2
+      // back y, pass 1: C1 = B_y^T A1 + Dd_y^T A2 -> W0; then A3 -> W1
       T c1[ND];
 #pragma unroll
       for (int i = 0; i < ND; ++i) c1[i] = T(0);
@@ -514,18 +511,18 @@ BDX_PRAGMA_UNROLL(QUnroll3<NQ>::value)
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
         for (int qy = 0; qy < NQ; ++qy) {
           T r1[ND], r2[ND];
-          ldrow<ND>(A1 + offA(c, qy, b), r1);
-          ldrow<ND>(A2 + offA(c, qy, b), r2);
+          ldrow<ND>(W0 + offA(c, qy, b), r1);
+          ldrow<ND>(W1 + offA(c, qy, b), r2);
           const T bq = bcj[qy], dq = dcj[qy];
 #pragma unroll
           for (int i = 0; i < ND; ++i) c1[i] += bq * r1[i] + dq * r2[i];
         }
       }
       wave_order();
-      if (lane_on && a < ND) strow<ND>(wB + offC(c, a, b), c1);
-      if (lane_on) strow<ND>(A3 + offA(c, a, b), a3);
+      if (lane_on && a < ND) strow<ND>(W0 + offA(c, a, b), c1);
+      if (lane_on) strow<ND>(W1 + offA(c, a, b), a3);
       cell_sync();
-      // pass 2: C3 = B_y^T A3 -> R2
+      // pass 2: C3 = B_y^T A3 -> W1
       T c3[ND];
 #pragma unroll
       for (int i = 0; i < ND; ++i) c3[i] = T(0);
@@ -534,38 +531,39 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
         for (int qy = 0; qy < NQ; ++qy) {
           T r3[ND];
-          ldrow<ND>(A3 + offA(c, qy, b), r3);
+          ldrow<ND>(W1 + offA(c, qy, b), r3);
           const T bq = bcj[qy];
 #pragma unroll
           for (int i = 0; i < ND; ++i) c3[i] += bq * r3[i];
         }
       }
       wave_order();
-      if (lane_on && a < ND) strow<ND>(wD + offC(c, a, b), c3);
+      if (lane_on && a < ND) strow<ND>(W1 + offA(c, a, b), c3);
       cell_sync();
     } else {
+      // A3 -> W2 (free since the previous layer's gather); A1, A2 -> W0, W1
+      // once every wave finished its front-y reads of them
+      if (lane_on) strow<ND>(W2 + offA(c, a, b), a3);
+      cell_sync();
       if (lane_on) {
-        const int o = offA(c, a, b);
-        strow<ND>(A1 + o, a1);
-        strow<ND>(A2 + o, a2);
-        strow<ND>(A3 + o, a3);
+        strow<ND>(W0 + offA(c, a, b), a1);
+        strow<ND>(W1 + offA(c, a, b), a2);
       }
       cell_sync();
       // back y: lanes (c, j = a < ND, qz = b): C1 = B_y^T A1 + Dd_y^T A2, C3 = B_y^T A3
-      // (into WB / WD: the front-y reads of this cell finished before the sync)
+      T c1[ND], c3[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) c1[i] = c3[i] = T(0);
       if (lane_on && a < ND) {
         const T* bcj = s_tab + OFF_BC + a * XP;
         const T* dcj = s_tab + OFF_DC + a * XP;
-        T c1[ND], c3[ND];
-#pragma unroll
-        for (int i = 0; i < ND; ++i) c1[i] = c3[i] = T(0);
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
         for (int qy = 0; qy < (BDX_X3_NOBY ? 0 : NQ); ++qy) {
           const int o = offA(c, qy, b);
           T r1[ND], r2[ND], r3[ND];
-          ldrow<ND>(A1 + o, r1);
-          ldrow<ND>(A2 + o, r2);
-          ldrow<ND>(A3 + o, r3);
+          ldrow<ND>(W0 + o, r1);
+          ldrow<ND>(W1 + o, r2);
+          ldrow<ND>(W2 + o, r3);
           const T bq = bcj[qy], dq = dcj[qy];
 #pragma unroll
           for (int i = 0; i < ND; ++i) {
@@ -573,9 +571,11 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
             c3[i] += bq * r3[i];
           }
         }
-        const int o = offC(c, a, b);
-        strow<ND>(wB + o, c1);
-        strow<ND>(wD + o, c3);
+      }
+      cell_sync();  // every wave's back-y reads done before C overwrites A1/A2
+      if (lane_on && a < ND) {
+        strow<ND>(W0 + offA(c, a, b), c1);
+        strow<ND>(W1 + offA(c, a, b), c3);
       }
       cell_sync();
     }
@@ -590,10 +590,10 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
       const T* dck = s_tab + OFF_DC + b * XP;
 BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
       for (int qz = 0; qz < (BDX_X3_NOBZ ? 0 : NQ); ++qz) {
-        const int o = offC(c, a, qz);
+        const int o = offA(c, a, qz);
         T r1[ND], r3[ND];
-        ldrow<ND>(wB + o, r1);
-        ldrow<ND>(wD + o, r3);
+        ldrow<ND>(W0 + o, r1);
+        ldrow<ND>(W1 + o, r3);
         const T bq = bck[qz], dq = dck[qz];
 #pragma unroll
         for (int i = 0; i < ND; ++i) ye[i] += bq * r1[i] + dq * r3[i];
@@ -615,7 +615,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
 #pragma unroll
         for (int i = 0; i < ND; ++i) ye[i] = T(0);
       }
-      strow<ND>(A1 + c * RW + (a * ND + b) * NP, ye);
+      strow<ND>((WAVELOCAL ? W0 : W2) + offA(c, a, b), ye);
     }
     __syncthreads();
 
