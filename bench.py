@@ -44,6 +44,8 @@ def parse_args(argv=None):
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--geometry", default="auto")
     ap.add_argument("--platform", default="gpu")
+    ap.add_argument("--kappa", default="constant", choices=["constant", "random"],
+                    help="per-cell random coefficients instead of the constant 2.0")
     return ap.parse_args(argv)
 
 
@@ -74,7 +76,7 @@ def run(comm, a) -> dict | None:
 
     t_setup = time.perf_counter()
     log(f"mesh {nx} degree {degree} fp{bits} on {n} rank(s)")
-    pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, 0.0)
+    pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, 0.0, a.kappa)
     log("problem built")
     u = pb.assemble_rhs()
     x = pb.new_vector()
@@ -136,6 +138,7 @@ def run(comm, a) -> dict | None:
             "mesh": list(nx),
             "kernel": getattr(op, "name", type(op).__name__),
             "geometry": getattr(op, "geometry", "otf"),
+            "kappa": a.kappa,
             "runtime": (f"native C++ ({op._rt.transport}, hipGraph={op._rt.graphs})"
                         if getattr(op, "_rt", None) is not None else "python"),
             "per_gpu_gdofs": value / n,

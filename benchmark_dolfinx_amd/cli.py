@@ -60,6 +60,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="Geometry factors on the fly (otf: constant-Jacobian fast path for "
                          "parallelepiped cells; otf-general: always the trilinear path) or "
                          "precomputed (stored, the reference's layout)")
+    ap.add_argument("--kappa", default="constant", choices=["constant", "random"],
+                    help="Diffusion coefficient: the reference's constant 2.0, or a random "
+                         "per-cell field U(1, 3) (partition-invariant)")
     ap.add_argument("--warmup", type=int, default=0,
                     help="Untimed repetitions before the timed loop")
     return ap
@@ -148,7 +151,7 @@ def run_benchmark(comm, nx, args, platform):
 
     dtype = torch.float64 if args.float == 64 else torch.float32
     pb = PoissonProblem(comm, nx, args.degree, args.qmode, args.use_gauss, dtype,
-                        platform, args.geom_perturb_fact)
+                        platform, args.geom_perturb_fact, args.kappa)
     res = laplace_action(pb, args.nreps, args.cg, args.mat_comp, kernel=args.kernel,
                          geometry=args.geometry, warmup=args.warmup)
     t = res.mat_free_time

@@ -58,6 +58,7 @@ struct Fused2Args {
   T* __restrict__ zb;
   T* __restrict__ cb;
   const T* __restrict__ xv;
+  const T* __restrict__ kc;    // per-cell coefficient [n0][n1][n2] or null (constant kappa)
   const double* __restrict__ scal;
   double* __restrict__ partials;
   int64_t ps;      // x-plane stride of the vectors (Ly * ld)
@@ -412,7 +413,11 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
     // G = kappa w_a w_b adj(J) adj(J)^T / det J is formed once per thread and
     // layer; per point only the weight w_q remains (same operator, same maths).
     T Gc[6] = {0, 0, 0, 0, 0, 0};
-    const T kwyz = A.kappa * s_qw[NQ + a] * s_qw[NQ + b];
+    const T kcell = A.kc ? (cell_on ? A.kc[(static_cast<int64_t>(cx) * A.n1 + ty * TY + cy) * A.n2 +
+                                          tz * TZ + cz]
+                                    : T(0))
+                         : A.kappa;
+    const T kwyz = kcell * s_qw[NQ + a] * s_qw[NQ + b];
     {
       const T* X0 = sX;
       const T* X1 = sX + NV;
@@ -749,7 +754,7 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
       int mode, int affine_ok, const int64_t* latd, int nq, const double* wts,     \
       const double* qpts,                                                          \
       const T* u, const T* pold, T* pnew, T* x, T* y, T* yb, T* zb, T* cb,         \
-      const T* xv, const T* tabs, double kappa, const double* scal,                \
+      const T* xv, const T* kc, const T* tabs, double kappa, const double* scal,   \
       double* partials, int beta_num, int beta_den, int xa_num, int xa_den,        \
       int nty, int ntz, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
@@ -763,6 +768,7 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
     a.zb = zb;                                                                     \
     a.cb = cb;                                                                     \
     a.xv = xv;                                                                     \
+    a.kc = kc;                                                                     \
     a.scal = scal;                                                                 \
     a.partials = partials;                                                         \
     a.beta_num = beta_num;                                                         \

@@ -398,7 +398,11 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
     // G = kappa w_a w_b adj(J) adj(J)^T / det J is formed once per thread and
     // layer; per point only the weight w_q remains (same operator, same maths).
     T Gc[6] = {0, 0, 0, 0, 0, 0};
-    const T kwyz = A.kappa * s_qw[NQ + a] * s_qw[NQ + b];
+    const T kcell = A.kc ? (cell_on ? A.kc[(static_cast<int64_t>(cx) * A.n1 + ty * TY + cy) * A.n2 +
+                                          tz * TZ + cz]
+                                    : T(0))
+                         : A.kappa;
+    const T kwyz = kcell * s_qw[NQ + a] * s_qw[NQ + b];
     {
       const T* X0 = sX;
       const T* X1 = sX + NV;
@@ -729,7 +733,7 @@ int launch_fused3(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, 
       int mode, int affine_ok, const int64_t* latd, int nq, const double* wts,     \
       const double* qpts,                                                          \
       const T* u, const T* pold, T* pnew, T* x, T* y, T* yb, T* zb, T* cb,         \
-      const T* xv, const T* tabs, double kappa, const double* scal,                \
+      const T* xv, const T* kc, const T* tabs, double kappa, const double* scal,   \
       double* partials, int beta_num, int beta_den, int xa_num, int xa_den,        \
       int nty, int ntz, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
@@ -743,6 +747,7 @@ int launch_fused3(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, 
     a.zb = zb;                                                                     \
     a.cb = cb;                                                                     \
     a.xv = xv;                                                                     \
+    a.kc = kc;                                                                     \
     a.scal = scal;                                                                 \
     a.partials = partials;                                                         \
     a.beta_num = beta_num;                                                         \

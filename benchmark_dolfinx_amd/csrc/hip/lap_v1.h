@@ -35,7 +35,8 @@ struct V1Shape {
 template <typename T, int ND, int NQ, int MODE, int GEOM>
 __global__ void __launch_bounds__(V1Shape<NQ>::threads)
     lap_v1_kernel(BdxLattice lat, OpTables<T> tb, const T* __restrict__ G,
-                  const T* __restrict__ xv, T kappa, const T* __restrict__ u,
+                  const T* __restrict__ xv, T kappa, const T* __restrict__ kc,
+                  const T* __restrict__ u,
                   T* __restrict__ y, int64_t lo0, int64_t lo1, int64_t lo2,
                   int64_t e0, int64_t e1, int64_t e2) {
   constexpr int nq3 = NQ * NQ * NQ;
@@ -143,9 +144,11 @@ __global__ void __launch_bounds__(V1Shape<NQ>::threads)
         geometry_G<T>(s_X[cs], tb.qpts[qx], tb.qpts[qy], tb.qpts[qz], w, Gd);
       }
     }
-    const T fx = kappa * (Gd[0] * gx + Gd[1] * gy + Gd[2] * gz);
-    const T fy = kappa * (Gd[1] * gx + Gd[3] * gy + Gd[4] * gz);
-    const T fz = kappa * (Gd[2] * gx + Gd[4] * gy + Gd[5] * gz);
+    // per-cell coefficient (random-coefficient runs) or the constant kappa
+    const T kap = (kc && valid) ? kc[cell_index(lat, cx, cy, cz)] : kappa;
+    const T fx = kap * (Gd[0] * gx + Gd[1] * gy + Gd[2] * gz);
+    const T fy = kap * (Gd[1] * gx + Gd[3] * gy + Gd[4] * gz);
+    const T fz = kap * (Gd[2] * gx + Gd[4] * gy + Gd[5] * gz);
     if (active) {
       s1[cs][q] = fx;
       s2[cs][q] = fy;

@@ -5,7 +5,7 @@
 
 template <typename T, int ND, int NQ, int MODE, int GEOM>
 int launch_v1(const BdxLattice& lat, const OpTables<T>& tb, const T* G,
-              const T* xv, T kappa, const T* u, T* y, const int64_t* lo,
+              const T* xv, T kappa, const T* kc, const T* u, T* y, const int64_t* lo,
               const int64_t* hi, hipStream_t st) {
   const int64_t e0 = hi[0] - lo[0], e1 = hi[1] - lo[1], e2 = hi[2] - lo[2];
   if (e0 <= 0 || e1 <= 0 || e2 <= 0) return 0;
@@ -15,22 +15,22 @@ int launch_v1(const BdxLattice& lat, const OpTables<T>& tb, const T* G,
   if (nblk > 0x7fffffffLL) return static_cast<int>(hipErrorInvalidValue);
   lap_v1_kernel<T, ND, NQ, MODE, GEOM>
       <<<static_cast<unsigned>(nblk), V1Shape<NQ>::threads, 0, st>>>(
-          lat, tb, G, xv, kappa, u, y, lo[0], lo[1], lo[2], e0, e1, e2);
+          lat, tb, G, xv, kappa, kc, u, y, lo[0], lo[1], lo[2], e0, e1, e2);
   return static_cast<int>(hipGetLastError());
 }
 
 template <typename T, int MODE, int GEOM>
 int dispatch_v1(int P, int nq, const BdxLattice& lat, const OpTables<T>& tb,
-                const T* G, const T* xv, T kappa, const T* u, T* y,
+                const T* G, const T* xv, T kappa, const T* kc, const T* u, T* y,
                 const int64_t* lo, const int64_t* hi, hipStream_t st) {
 #define BDX_V1_CASE(PP)                                                    \
   case PP:                                                                 \
     if (nq == PP + 1)                                                      \
       return launch_v1<T, PP + 1, PP + 1, MODE, GEOM>(lat, tb, G, xv, kappa, \
-                                                      u, y, lo, hi, st);   \
+                                                      kc, u, y, lo, hi, st); \
     if (nq == PP + 2)                                                      \
       return launch_v1<T, PP + 1, PP + 2, MODE, GEOM>(lat, tb, G, xv, kappa, \
-                                                      u, y, lo, hi, st);   \
+                                                      kc, u, y, lo, hi, st); \
     break;
   switch (P) {
     BDX_V1_CASE(1)
@@ -50,7 +50,8 @@ int dispatch_v1(int P, int nq, const BdxLattice& lat, const OpTables<T>& tb,
   extern "C" int bdx_v1_apply_##SUF(                                           \
       int mode, const int64_t* latd, int nq, const double* phi0,               \
       const double* dphi1, const double* wts, const double* qpts,              \
-      int identity, const T* G, const T* xv, double kappa, const T* u, T* y,   \
+      int identity, const T* G, const T* xv, double kappa, const T* kc,        \
+      const T* u, T* y,                                                        \
       const int64_t* lo, const int64_t* hi, hipStream_t st) {                  \
     const BdxLattice lat = BdxLattice::from(latd);                             \
     const int P = static_cast<int>(lat.P);                                     \
@@ -59,10 +60,10 @@ int dispatch_v1(int P, int nq, const BdxLattice& lat, const OpTables<T>& tb,
     const T k = static_cast<T>(kappa);                                         \
     if (mode == 0)                                                             \
       return dispatch_v1<T, kModeStiffness, kGeomStored>(P, nq, lat, tb, G, xv, \
-                                                         k, u, y, lo, hi, st); \
+                                                         k, kc, u, y, lo, hi, st); \
     if (mode == 1)                                                             \
       return dispatch_v1<T, kModeStiffness, kGeomOTF>(P, nq, lat, tb, G, xv, k, \
-                                                      u, y, lo, hi, st);       \
-    return dispatch_v1<T, kModeMass, kGeomOTF>(P, nq, lat, tb, G, xv, k, u, y, \
-                                               lo, hi, st);                    \
+                                                      kc, u, y, lo, hi, st);   \
+    return dispatch_v1<T, kModeMass, kGeomOTF>(P, nq, lat, tb, G, xv, k, nullptr, \
+                                               u, y, lo, hi, st);              \
   }

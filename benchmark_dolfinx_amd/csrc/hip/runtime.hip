@@ -58,8 +58,8 @@ int bdx_xflush_f32(const int64_t*, const int64_t*, float*, const float*, const d
 #define BDX_DECL_APPLY(V, T, SUF, PP)                                                        \
   extern "C" __attribute__((weak)) int bdx_fused##V##_apply_##SUF##_p##PP(                  \
       int, int, const int64_t*, int, const double*, const double*, const T*, const T*, T*, \
-      T*, T*, T*, T*, T*, const T*, const T*, double, const double*, double*, int, int, int, \
-      int, int, int, hipStream_t);
+      T*, T*, T*, T*, T*, const T*, const T*, const T*, double, const double*, double*, int, \
+      int, int, int, int, int, hipStream_t);
 #define BDX_DECL_ALL(V)                                                                    \
   BDX_DECL_APPLY(V, double, f64, 1) BDX_DECL_APPLY(V, double, f64, 2)                      \
   BDX_DECL_APPLY(V, double, f64, 3) BDX_DECL_APPLY(V, double, f64, 4)                      \
@@ -75,7 +75,7 @@ namespace {
 
 template <typename T>
 using ApplyFn = int (*)(int, int, const int64_t*, int, const double*, const double*, const T*,
-                        const T*, T*, T*, T*, T*, T*, T*, const T*, const T*, double,
+                        const T*, T*, T*, T*, T*, T*, T*, const T*, const T*, const T*, double,
                         const double*, double*, int, int, int, int, int, int, hipStream_t);
 
 template <typename T>
@@ -231,6 +231,7 @@ struct CGRuntime {
   std::vector<T> tabs;
   T *x, *r, *pa, *pb, *y, *yb, *zb, *cb;
   const T* xv;
+  const T* kc = nullptr;
   double *scal, *partials, *upart;
   // halo: owned lower faces <-> ghost planes (parallel/halo.py layout)
   bool halo = false;
@@ -273,7 +274,7 @@ struct CGRuntime {
     int rc;
     if (halo && (rc = halo_forward(r))) return rc;
     rc = apply(1, cfg.affine, cfg.latd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold, pnew,
-               x, y, yb, zb, cb, xv, tabs.data(), cfg.kappa, scal, partials,
+               x, y, yb, zb, cb, xv, kc, tabs.data(), cfg.kappa, scal, partials,
                first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1, cfg.nty,
                cfg.ntz, st);
     if (rc) return rc;
@@ -421,6 +422,7 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   rt->hbuf_b = static_cast<T*>(ptrs[i++]);
   rt->face_boxes = static_cast<const int64_t*>(ptrs[i++]);
   rt->ghost_boxes = static_cast<const int64_t*>(ptrs[i++]);
+  rt->kc = static_cast<const T*>(ptrs[i++]);
   rt->nface_boxes = static_cast<int>(halo_sizes[0]);
   rt->face_total = halo_sizes[1];
   rt->nghost_boxes = static_cast<int>(halo_sizes[2]);

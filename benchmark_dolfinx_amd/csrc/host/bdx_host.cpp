@@ -152,8 +152,9 @@ inline void interp_t(const Tables<T>& tb, const T* r, T* ye, T* t1, T* t2) {
 // get y = u (only on the owning rank).
 template <typename T, int ND, int NQ>
 void stiffness_cell(const BdxLattice& lat, const Tables<T>& tb, const T* xv,
-                    T kappa, const T* u, T* y, int64_t cx, int64_t cy,
+                    T kappa, const T* kc, const T* u, T* y, int64_t cx, int64_t cy,
                     int64_t cz) {
+  if (kc) kappa = kc[(cx * lat.n[1] + cy) * lat.n[2] + cz];  // per-cell coefficient
   constexpr int nd3 = ND * ND * ND, nq3 = NQ * NQ * NQ;
   const int64_t P = lat.P;
   T ue[nd3];
@@ -284,6 +285,7 @@ struct StiffArgs {
   Tables<T> tb;
   const T* xv;
   T kappa;
+  const T* kc;
   const T* u;
   T* y;
   int64_t lo[3], hi[3];
@@ -295,8 +297,8 @@ struct Stiff {
   struct K {
     static void run(const StiffArgs<T>& a) {
       for_cells(a.lo, a.hi, [&](int64_t cx, int64_t cy, int64_t cz) {
-        stiffness_cell<T, ND, NQ>(a.lat, a.tb, a.xv, a.kappa, a.u, a.y, cx, cy,
-                                  cz);
+        stiffness_cell<T, ND, NQ>(a.lat, a.tb, a.xv, a.kappa, a.kc, a.u, a.y, cx,
+                                  cy, cz);
       });
     }
   };
@@ -343,7 +345,7 @@ inline void col_range(int64_t i, int64_t P, int64_t n, int64_t& lo,
 
 template <typename T>
 int64_t csr_build(const int64_t* latd, int nq, const T* B, const T* Dd,
-                  const T* wts, const T* qpts, const T* xv, T kappa,
+                  const T* wts, const T* qpts, const T* xv, T kappa, const T* kc,
                   int64_t* row_ptr, int32_t* cols, T* vals, int count_only) {
   const BdxLattice lat = BdxLattice::from(latd);
   const int64_t P = lat.P, nd = P + 1;
@@ -404,6 +406,7 @@ int64_t csr_build(const int64_t* latd, int nq, const T* B, const T* Dd,
   for_cells(lo0, hi0, [&](int64_t cx, int64_t cy, int64_t cz) {
     T X[8][3];
     cell_vertices(lat, xv, cx, cy, cz, X);
+    const T kap = kc ? kc[(cx * lat.n[1] + cy) * lat.n[2] + cz] : kappa;
     std::vector<T> Gq(static_cast<size_t>(nq3) * 6);
     for (int qx = 0; qx < nq; ++qx)
       for (int qy = 0; qy < nq; ++qy)
@@ -418,9 +421,9 @@ int64_t csr_build(const int64_t* latd, int nq, const T* B, const T* Dd,
         const T* g = &gref[(static_cast<size_t>(b) * nq3 + q) * 3];
         const T* G = &Gq[6 * q];
         T* t = &tmp[(static_cast<size_t>(b) * nq3 + q) * 3];
-        t[0] = kappa * (G[0] * g[0] + G[1] * g[1] + G[2] * g[2]);
-        t[1] = kappa * (G[1] * g[0] + G[3] * g[1] + G[4] * g[2]);
-        t[2] = kappa * (G[2] * g[0] + G[4] * g[1] + G[5] * g[2]);
+        t[0] = kap * (G[0] * g[0] + G[1] * g[1] + G[2] * g[2]);
+        t[1] = kap * (G[1] * g[0] + G[3] * g[1] + G[4] * g[2]);
+        t[2] = kap * (G[2] * g[0] + G[4] * g[1] + G[5] * g[2]);
       }
     for (int a = 0; a < nd3; ++a) {
       const int ia = a / static_cast<int>(nd * nd),
@@ -471,13 +474,14 @@ int bdx_host_version() { return 1; }
   void bdx_cpu_stiffness_##SUF(const int64_t* latd, int nq, const T* phi0,    \
                                const T* dphi1, const T* wts, const T* qpts,   \
                                const T* nodes, int identity, const T* xv,     \
-                               T kappa, const T* u, T* y, const int64_t* lo,  \
-                               const int64_t* hi) {                           \
+                               T kappa, const T* kc, const T* u, T* y,        \
+                               const int64_t* lo, const int64_t* hi) {        \
     StiffArgs<T> a;                                                           \
     a.lat = BdxLattice::from(latd);                                           \
     a.tb = make_tables<T>(phi0, dphi1, wts, qpts, nodes, identity);           \
     a.xv = xv;                                                                \
     a.kappa = kappa;                                                          \
+    a.kc = kc;                                                                \
     a.u = u;                                                                  \
     a.y = y;                                                                  \
     for (int d = 0; d < 3; ++d) {                                             \
@@ -505,10 +509,11 @@ int bdx_host_version() { return 1; }
   }                                                                           \
   int64_t bdx_cpu_csr_##SUF(const int64_t* latd, int nq, const T* B,          \
                             const T* Dd, const T* wts, const T* qpts,         \
-                            const T* xv, T kappa, int64_t* row_ptr,           \
-                            int32_t* cols, T* vals, int count_only) {         \
-    return csr_build<T>(latd, nq, B, Dd, wts, qpts, xv, kappa, row_ptr, cols, \
-                        vals, count_only);                                    \
+                            const T* xv, T kappa, const T* kc,                \
+                            int64_t* row_ptr, int32_t* cols, T* vals,         \
+                            int count_only) {                                 \
+    return csr_build<T>(latd, nq, B, Dd, wts, qpts, xv, kappa, kc, row_ptr,   \
+                        cols, vals, count_only);                              \
   }                                                                           \
   void bdx_cpu_spmv_##SUF(int64_t nrows, const int64_t* row_ptr,              \
                           const int32_t* cols, const T* vals, const T* x,     \

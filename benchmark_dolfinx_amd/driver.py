@@ -39,7 +39,7 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         # (Q3 +4 %, Q6 +12 % over fused2); on general trilinear meshes its
         # larger register footprint spills at Q3, so fused2 takes those
         if geometry == "stored":
-            kernel = "fused"
+            kernel = "fused" if pb.kc is None else "v1"
         elif geometry == "otf-general" or not pb.all_affine:
             kernel = "fused2"
         else:
@@ -60,7 +60,7 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         geometry = "otf"
     if kernel == "fused":
         from .models.fused import FusedLaplacianGPU, fused_supported
-        if fused_supported(pb):
+        if fused_supported(pb) and pb.kc is None:
             return FusedLaplacianGPU(pb, geometry="otf" if geometry == "auto" else geometry)
         kernel = "v1"
     if kernel == "v1":

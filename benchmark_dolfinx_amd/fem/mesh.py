@@ -315,3 +315,21 @@ def _hash_uniform(ids: np.ndarray, seed: int) -> np.ndarray:
 
 def cells_per_dof_estimate(degree: int) -> float:
     return 1.0 / math.pow(degree, 3)
+
+
+def cell_coefficients(lat: LocalLattice, mode: str = "constant", kappa: float = 2.0,
+                      seed: int = 7):
+    """Per-cell diffusion coefficient of the local cells, shape (n0, n1, n2), or
+    None for the reference's constant kappa (src/main.cpp:71; the reference
+    stores it per cell, src/laplacian.hpp:105).  mode="random": kappa_c =
+    U(1, 3) from a counter-based hash of the *global* cell id, so every
+    partition sees the same field."""
+    if mode == "constant":
+        return None
+    if mode != "random":
+        raise ValueError(f"unknown coefficient mode {mode}")
+    nxg, nyg, nzg = lat.ncells_global
+    gid = ((np.arange(lat.c0[0], lat.c1[0], dtype=np.uint64)[:, None, None] * np.uint64(nyg)
+            + np.arange(lat.c0[1], lat.c1[1], dtype=np.uint64)[None, :, None]) * np.uint64(nzg)
+           + np.arange(lat.c0[2], lat.c1[2], dtype=np.uint64)[None, None, :])
+    return 1.0 + 2.0 * _hash_uniform(gid, seed)

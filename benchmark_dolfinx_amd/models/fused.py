@@ -48,6 +48,8 @@ class FusedLaplacianGPU:
             raise ValueError(f"unknown geometry mode {geometry}")
         if version >= 2 and geometry != "otf":
             raise ValueError("fused2/3 support on-the-fly geometry only")
+        if version == 1 and pb.kc is not None:
+            raise ValueError("the fused v1 kernel has no per-cell coefficients; use fused2/3 or v1")
         self.version = version
         # CG loop driver for fused2/3: "native" = C++ runtime (solvers/native.py),
         # "python" = the launch sequence below driven from Python
@@ -120,7 +122,7 @@ class FusedLaplacianGPU:
             _check(self._apply2(mode, int(self.affine), ptr(pb.latd), t.nq, ptr(t.wts),
                                 ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(x), ptr(y),
                                 ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(pb.xv),
-                                ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials),
+                                ptr(pb.kc), ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials),
                                 beta_num, beta_den, xa_num, xa_den, self.nty, self.ntz,
                                 _stream()), "fused2_apply")
         else:

@@ -21,7 +21,8 @@ import math
 import numpy as np
 import torch
 
-from ..fem.mesh import LocalLattice, make_local_lattice, vertex_coordinates
+from ..fem.mesh import (LocalLattice, cell_coefficients, make_local_lattice,
+                        vertex_coordinates)
 from ..fem.quadrature import OperatorTables
 from ..ops import native
 from ..ops.native import ptr
@@ -59,7 +60,7 @@ def cells_all_parallelepipeds(X: np.ndarray) -> bool:
 class PoissonProblem:
     def __init__(self, comm: Comm, ncells, degree: int, qmode: int = 1,
                  use_gauss: bool = False, dtype=torch.float64, platform: str = "gpu",
-                 perturb: float = 0.0):
+                 perturb: float = 0.0, coefficient: str = "constant"):
         if use_gauss and qmode == 0:
             # same validation as the reference (src/laplacian.hpp:197-198, Q5)
             raise RuntimeError("Expecting identity matrix for qmode=0")
@@ -91,6 +92,11 @@ class PoissonProblem:
         # kept alive for ctypes calls (never pass temporaries to ptr())
         self.latd = self.lat.as_int64()
         self.all_affine = cells_all_parallelepipeds(self.xv_host)
+        # per-cell kappa (None: the reference's constant kappa = 2)
+        self.coefficient = coefficient
+        kc = cell_coefficients(self.lat, coefficient, KAPPA)
+        self.kc_host = None if kc is None else np.ascontiguousarray(kc, dtype=npdt)
+        self.kc = None if kc is None else torch.from_numpy(self.kc_host).to(self.device)
 
     # --------------------------------------------------------------- vectors
     @property
@@ -211,7 +217,7 @@ class MatFreeLaplacianCPU:
         self._fn(ptr(self.latd), self.pb.tables.nq, ptr(t["phi0"]), ptr(t["dphi1"]),
                  ptr(t["wts"]), ptr(t["qpts"]), ptr(t["nodes"]),
                  int(self.pb.tables.is_identity), ptr(self.pb.xv_host), self.pb.kappa,
-                 ptr(u.numpy()), ptr(y.numpy()), ptr(lo), ptr(hi))
+                 ptr(self.pb.kc_host), ptr(u.numpy()), ptr(y.numpy()), ptr(lo), ptr(hi))
 
     def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
         lat = self.pb.lat
@@ -254,10 +260,10 @@ class MatFreeLaplacianGPU:
         y.zero_()
         work = pb.halo.forward_begin(u)
         lo, hi = lat.interior_cell_box()
-        self.k.v1_apply(self.mode, self.G, pb.xv, pb.kappa, u, y, lo, hi)
+        self.k.v1_apply(self.mode, self.G, pb.xv, pb.kappa, u, y, lo, hi, pb.kc)
         pb.halo.forward_end(u, work)
         for lo, hi in lat.boundary_cell_boxes():
-            self.k.v1_apply(self.mode, self.G, pb.xv, pb.kappa, u, y, lo, hi)
+            self.k.v1_apply(self.mode, self.G, pb.xv, pb.kappa, u, y, lo, hi, pb.kc)
         pb.halo.reverse(y)
 
 
@@ -282,7 +288,8 @@ class CSROperator:
         row_ptr = np.zeros(lat.nstore + 1, dtype=np.int64)
         self.latd = problem.latd
         args = (ptr(self.latd), problem.tables.nq, ptr(t["B"]), ptr(t["Dd"]),
-                ptr(t["wts"]), ptr(t["qpts"]), ptr(problem.xv_host), problem.kappa)
+                ptr(t["wts"]), ptr(t["qpts"]), ptr(problem.xv_host), problem.kappa,
+                ptr(problem.kc_host))
         with timed("% Create CPU MatrixCSR"):
             nnz = fn(*args, ptr(row_ptr), 0, 0, 1)
             if nnz >= 2 ** 31:

@@ -29,7 +29,7 @@ def declare(lib) -> None:
         _d(lib, f"bdx_axpy_{suf}", [i64, i64, i64, i64, i64, vp, f64, vp, vp, vp])
         _d(lib, f"bdx_box_copy_{suf}", [i32, vp, i64, i64, vp, i32, i64, vp, vp])
         _d(lib, f"bdx_v1_apply_{suf}",
-           [i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp])
+           [i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp, vp])
         _d(lib, f"bdx_geometry_{suf}", [vp, i32, vp, vp, vp, vp, vp, vp, vp])
         _d(lib, f"bdx_spmv_{suf}", [i64, vp, vp, vp, vp, vp, vp])
         for P in range(1, 8):
@@ -41,7 +41,7 @@ def declare(lib) -> None:
             name = f"bdx_fused{v}_apply_{suf}_p{P}"
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
-                               vp, f64, vp, vp, i32, i32, i32, i32, i32, i32, vp])
+                               vp, vp, f64, vp, vp, i32, i32, i32, i32, i32, i32, vp])
         _d(lib, f"bdx_fused_finalize_{suf}", [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp])
         _d(lib, f"bdx_cg_update_iface_{suf}", [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32,
                                                 vp, i32, i32, i32, vp, vp])

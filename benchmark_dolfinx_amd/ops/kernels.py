@@ -61,13 +61,13 @@ class HipKernels:
         return getattr(self.lib, f"{name}_{self.suf}")
 
     # --------------------------------------------------------------- operator
-    def v1_apply(self, mode: int, G, xv, kappa: float, u, y, lo, hi):
+    def v1_apply(self, mode: int, G, xv, kappa: float, u, y, lo, hi, kc=None):
         lo = np.asarray(lo, dtype=np.int64)
         hi = np.asarray(hi, dtype=np.int64)
         t = self.t
         _check(self._f("bdx_v1_apply")(mode, ptr(self.latd), t.nq, ptr(t.phi0),
                                        ptr(t.dphi1), ptr(t.wts), ptr(t.qpts), t.identity,
-                                       ptr(G), ptr(xv), kappa, ptr(u), ptr(y), ptr(lo),
+                                       ptr(G), ptr(xv), kappa, ptr(kc), ptr(u), ptr(y), ptr(lo),
                                        ptr(hi), _stream()), "v1_apply")
 
     def geometry(self, xv, G):

@@ -62,11 +62,11 @@ def host():
             lib = ctypes.CDLL(str(path))
             for suf, ft in (("f64", f64), ("f32", f32)):
                 _declare(lib, f"bdx_cpu_stiffness_{suf}",
-                         [vp, i32, vp, vp, vp, vp, vp, i32, vp, ft, vp, vp, vp, vp])
+                         [vp, i32, vp, vp, vp, vp, vp, i32, vp, ft, vp, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_mass_{suf}",
                          [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_csr_{suf}",
-                         [vp, i32, vp, vp, vp, vp, vp, ft, vp, vp, vp, i32], i64)
+                         [vp, i32, vp, vp, vp, vp, vp, ft, vp, vp, vp, vp, i32], i64)
                 _declare(lib, f"bdx_cpu_spmv_{suf}", [i64, vp, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_interp_f_{suf}", [vp, vp, vp, vp])
             _host = lib

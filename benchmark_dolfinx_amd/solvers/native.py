@@ -50,7 +50,7 @@ class NativeCGRuntime:
         self.upart = torch.zeros(2048, dtype=torch.float64, device=pb.device)
         fo, gh = halo.owned_faces, halo.ghosts
         bufs = [cg.x, cg.r, op.p_old, op.p_new, cg.y, op.yb, op.zb, op.cb, pb.xv, cg.scal,
-                op.partials, self.upart, halo.buf_a, halo.buf_b, fo.table, gh.table]
+                op.partials, self.upart, halo.buf_a, halo.buf_b, fo.table, gh.table, pb.kc]
         self._keep = bufs
         self._ptrs = (ctypes.c_void_p * len(bufs))(*[ptr(b) for b in bufs])
         self._hs = np.array([len(fo.boxes), fo.total, len(gh.boxes), gh.total], dtype=np.int64)

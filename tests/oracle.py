@@ -38,8 +38,9 @@ def _ref_grad_tables(t: OperatorTables):
     return np.transpose(g, (1, 0, 2)), val.T  # (a, q, 3), (a, q)
 
 
-def box_model(ncells, degree, qmode=1, use_gauss=False, vertices=None):
-    """Return dict(u, y, b, bc, N) on the global lattice (z fastest)."""
+def box_model(ncells, degree, qmode=1, use_gauss=False, vertices=None, kappa_cells=None):
+    """Return dict(u, y, b, bc, N) on the global lattice (z fastest).
+    kappa_cells: optional per-cell coefficient (nx, ny, nz); default KAPPA."""
     t = OperatorTables(degree, qmode, use_gauss)
     nx, ny, nz = ncells
     P = degree
@@ -93,10 +94,13 @@ def box_model(ncells, degree, qmode=1, use_gauss=False, vertices=None):
     b[bc] = 0.0
     u = b.copy()
 
+    kap = (np.full(C, KAPPA) if kappa_cells is None
+           else np.asarray(kappa_cells, dtype=np.float64).reshape(-1))
+
     def apply(x):
         xe = np.where(bc[dofs], 0.0, x[dofs])
         gu = np.einsum("aqd,ca->cqd", gref, xe)
-        Fq = KAPPA * np.einsum("cqde,cqe->cqd", G, gu)
+        Fq = kap[:, None, None] * np.einsum("cqde,cqe->cqd", G, gu)
         ye = np.einsum("aqd,cqd->ca", gref, Fq)
         ye = np.where(bc[dofs], 0.0, ye)
         y = np.zeros_like(x)

@@ -181,3 +181,42 @@ def test_norms_and_blas1(R):
         assert abs(r[1] - ref[1]) < 1e-14 * ref[1]   # linf = max |v| (not |max v|)
         assert r[2] < 1e-15
         assert abs(r[3] - r[4]) < 1e-12 * r[4]          # sum(u*u) == ||u||^2
+
+
+@pytest.mark.parametrize("nc,P,qm,pert", [((3, 2, 4), 2, 1, 0.0), ((2, 3, 2), 3, 0, 0.2),
+                                          ((2, 2, 2), 4, 1, 0.1)])
+def test_random_coefficients_vs_oracle(nc, P, qm, pert):
+    from benchmark_dolfinx_amd.fem.mesh import cell_coefficients
+    pb = PoissonProblem(Comm(), nc, P, qm, False, torch.float64, "cpu", pert, "random")
+    kc = cell_coefficients(make_local_lattice(0, 1, nc, P), "random")
+    assert kc.shape == nc and kc.min() >= 1.0 and kc.max() < 3.0 and kc.std() > 0.1
+    ref = oracle.box_model(nc, P, qm, vertices=_global_vertices(nc, pert), kappa_cells=kc)
+    rng = np.random.default_rng(11)
+    xg = rng.standard_normal(ref["u"].size)
+    x = pb.new_vector()
+    x[:, :, : pb.lat.L[2]] = torch.from_numpy(xg[pb.lat.global_indices()])
+    y = pb.new_vector()
+    MatFreeLaplacianCPU(pb).apply(x, y)
+    yr = ref["apply"](xg)
+    assert np.abs(pb.to_global_array(y) - yr).max() <= 1e-11 * np.abs(yr).max()
+    z = pb.new_vector()
+    CSROperator(pb).apply(x, z)
+    assert np.abs(pb.to_global_array(z) - yr).max() <= 1e-11 * np.abs(yr).max()
+
+
+@pytest.mark.parametrize("R", [2, 4])
+def test_random_coefficients_partition_invariant(R):
+    def body(comm):
+        pb = _problem((5, 4, 6), 2, 1, pert=0.1, comm=comm)
+        pb2 = PoissonProblem(comm, (5, 4, 6), 2, 1, False, torch.float64, "cpu", 0.1, "random")
+        u = pb2.assemble_rhs()
+        y = pb2.new_vector()
+        MatFreeLaplacianCPU(pb2).apply(u, y)
+        x = pb2.new_vector()
+        cg_solve(MatFreeLaplacianCPU(pb2), pb2, x, u, 6)
+        del pb
+        return pb2.norm(y), pb2.norm(x)
+
+    ref = body(Comm())
+    for r in run_threaded(R, body):
+        assert abs(r[0] - ref[0]) < 1e-12 * ref[0] and abs(r[1] - ref[1]) < 1e-10 * ref[1]

@@ -142,3 +142,28 @@ def test_fused3_cg_all_degrees(P, nc, pert):
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 12)
     rel = (cpu.owned(xg.cpu()) - cpu.owned(xc)).abs().max().item() / xc.abs().max().item()
     assert rel < 1e-10, rel
+
+
+@pytest.mark.parametrize("kernel", ["fused3", "fused2", "v1"])
+@pytest.mark.parametrize("nc,P,pert", [((4, 5, 7), 3, 0.0), ((3, 4, 5), 6, 0.1), ((5, 6, 6), 2, 0.0)])
+def test_random_coefficients_gpu(kernel, nc, P, pert):
+    """Per-cell random kappa: GPU kernels vs the C++ CPU operator, and CG."""
+    from benchmark_dolfinx_amd.driver import make_operator
+    gpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "gpu", pert, "random")
+    cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", pert, "random")
+    rng = np.random.default_rng(5)
+    u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
+    yc = cpu.new_vector()
+    MatFreeLaplacianCPU(cpu).apply(u64, yc)
+    op = make_operator(gpu, kernel)
+    yg = gpu.new_vector()
+    op.apply(u64.to(gpu.device), yg)
+    o = cpu.owned
+    err = (o(yg.cpu()) - o(yc)).abs().max().item()
+    assert err <= 1e-11 * yc.abs().max().item(), err
+    xg = gpu.new_vector()
+    DeviceCG(gpu).solve(op, xg, gpu.assemble_rhs(), 10)
+    xc = cpu.new_vector()
+    cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 10)
+    rel = (o(xg.cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
+    assert rel < 1e-10, rel
