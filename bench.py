@@ -111,6 +111,10 @@ def run(comm, a) -> dict | None:
     dt = comm.allreduce_scalar(dt, "max")
     value = pb.ndofs_global * a.steps / (1e9 * dt)
     ynorm = pb.norm(x)
+    runtime = (f"native C++ ({op._rt.transport}, hipGraph={op._rt.graphs})"
+               if getattr(op, "_rt", None) is not None else "python")
+    if hasattr(op, "close"):
+        op.close()
     if comm.rank != 0:
         return None
     px, py, pz = pb.lat.pgrid
@@ -139,8 +143,7 @@ def run(comm, a) -> dict | None:
             "kernel": getattr(op, "name", type(op).__name__),
             "geometry": getattr(op, "geometry", "otf"),
             "kappa": a.kappa,
-            "runtime": (f"native C++ ({op._rt.transport}, hipGraph={op._rt.graphs})"
-                        if getattr(op, "_rt", None) is not None else "python"),
+            "runtime": runtime,
             "per_gpu_gdofs": value / n,
             "y_norm": ynorm,
             "setup_s": t_setup,

@@ -161,7 +161,11 @@ template <int NQ> struct TileFor;
 template <> struct TileFor<2> { static constexpr int TY = 8, TZ = 8; };
 template <> struct TileFor<3> { static constexpr int TY = 4, TZ = 7; };
 template <> struct TileFor<4> { static constexpr int TY = 4, TZ = 4; };
-template <> struct TileFor<5> { static constexpr int TY = 2, TZ = 5; };
+#ifndef BDX_TILE5_TY
+#define BDX_TILE5_TY 2
+#define BDX_TILE5_TZ 5
+#endif
+template <> struct TileFor<5> { static constexpr int TY = BDX_TILE5_TY, TZ = BDX_TILE5_TZ; };
 template <> struct TileFor<6> { static constexpr int TY = 1, TZ = 7; };
 template <> struct TileFor<7> { static constexpr int TY = 1, TZ = 5; };
 template <> struct TileFor<8> { static constexpr int TY = 2, TZ = 2; };

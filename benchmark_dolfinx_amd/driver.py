@@ -141,4 +141,6 @@ def laplace_action(pb: PoissonProblem, nreps: int, use_cg: bool, mat_comp: bool,
             printer(f"Norm of error = {res.enorm:.6g}")
             rel = res.enorm / res.znorm if res.znorm != 0 else float("nan")
             printer(f"Relative norm of error = {rel:.6g}")
+    if hasattr(op, "close"):
+        op.close()  # native runtime: release RCCL / graphs before shutdown
     return res

@@ -109,6 +109,13 @@ class FusedLaplacianGPU:
         self.p_old = None
         self.p_new = None
 
+    def close(self) -> None:
+        """Release the native runtime (RCCL communicator, graphs, stream)
+        before the process group / HIP runtime shut down."""
+        if self._rt is not None:
+            self._rt.close()
+            self._rt = None
+
     # ------------------------------------------------------------ launches
     def _finalize(self, y, ghost_only: bool = False):
         _check(self._final(ptr(self.pb.latd), ptr(y), ptr(self.yb), ptr(self.zb), ptr(self.cb),
