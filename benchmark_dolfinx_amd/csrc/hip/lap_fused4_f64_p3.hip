@@ -1,0 +1,50 @@
+// Fused v4 operator kernels (MFMA core), double, degree 3.
+#include "lap_fused4.h"
+
+extern "C" int bdx_fused4_apply_f64_p3(
+    int mode, int affine_ok, const int64_t* latd, int nq, const double* wts, const double* qpts,
+    const double* u, const double* pold, double* pnew, double* x, double* y, double* yb,
+    double* zb, double* cb, const double* xv, const double* kc, const double* tabs, double kappa,
+    const double* scal, double* partials, int beta_num, int beta_den, int xa_num, int xa_den,
+    int nty, int ntz, hipStream_t st) {
+  (void)wts;
+  (void)qpts;
+  (void)nq;
+  // the Kronecker factorisation needs a constant Jacobian per cell
+  if (!affine_ok || !tabs) return static_cast<int>(hipErrorInvalidValue);
+  Fused2Args<double> a;
+  BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));
+  a.u = u;
+  a.pold = pold;
+  a.pnew = pnew;
+  a.x = x;
+  a.y = y;
+  a.yb = yb;
+  a.zb = zb;
+  a.cb = cb;
+  a.xv = xv;
+  a.kc = kc;
+  a.scal = scal;
+  a.partials = partials;
+  a.beta_num = beta_num;
+  a.beta_den = beta_den;
+  a.xa_num = xa_num;
+  a.xa_den = xa_den;
+  a.kappa = kappa;
+  FusedTables<double> tb;
+  for (int i = 0; i < kFusedTabMax; ++i) tb.tab[i] = tabs[i];
+  for (int q = 0; q < kMaxNq; ++q) tb.qpts[q] = tb.wts[q] = 0.0;
+  return mode == kFusedCG ? launch_fused4<kFusedCG>(a, tb, st)
+                          : launch_fused4<kFusedAction>(a, tb, st);
+}
+
+extern "C" int bdx_fused4_tables_f64(int nd, int nq, const double* phi0, const double* Dd,
+                                     const double* wts, double* out) {
+  return pack_tables4(nd, nq, phi0, Dd, wts, out);
+}
+
+extern "C" int bdx_fused4_tile(int* ty, int* tz) {
+  *ty = BDX_F4_TY;
+  *tz = BDX_F4_TZ;
+  return 0;
+}

@@ -70,6 +70,7 @@ int bdx_xflush_f32(const int64_t*, const int64_t*, float*, const float*, const d
   BDX_DECL_APPLY(V, float, f32, 6) BDX_DECL_APPLY(V, float, f32, 7)
 BDX_DECL_ALL(2)
 BDX_DECL_ALL(3)
+BDX_DECL_APPLY(4, double, f64, 3)
 
 namespace {
 
@@ -86,7 +87,7 @@ ApplyFn<double> apply_fn<double>(int version, int P) {
   if (version == V && P == PP) return bdx_fused##V##_apply_f64_p##PP;
   BDX_CASE(2, 1) BDX_CASE(2, 2) BDX_CASE(2, 3) BDX_CASE(2, 4) BDX_CASE(2, 5) BDX_CASE(2, 6)
   BDX_CASE(2, 7) BDX_CASE(3, 1) BDX_CASE(3, 2) BDX_CASE(3, 3) BDX_CASE(3, 4) BDX_CASE(3, 5)
-  BDX_CASE(3, 6) BDX_CASE(3, 7)
+  BDX_CASE(3, 6) BDX_CASE(3, 7) BDX_CASE(4, 3)
 #undef BDX_CASE
   return nullptr;
 }

@@ -10,6 +10,7 @@ the MAX over ranks (the reference reads rank 0's clock with no barrier).
 
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -43,7 +44,12 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         elif geometry == "otf-general" or not pb.all_affine:
             kernel = "fused2"
         else:
-            kernel = "fused3"
+            kernel = os.environ.get("BDX_AUTO_AFFINE", "fused3")
+    if kernel == "fused4":
+        from .models.fused import FusedLaplacianGPU, fused_supported
+        if fused_supported(pb, 4) and geometry in ("auto", "otf"):
+            return FusedLaplacianGPU(pb, geometry="otf", version=4)
+        kernel = "fused3"
     if kernel == "fused3":
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 3) and geometry in ("auto", "otf", "otf-general"):

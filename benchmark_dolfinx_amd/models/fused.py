@@ -33,6 +33,8 @@ def fused_supported(pb, version: int = 1) -> bool:
     lib = native.hip()
     if version == 3 and pb.tables.is_identity:
         return False  # fused3 is the phi0 != I core
+    if version == 4 and not pb.all_affine:
+        return False  # fused4's Kronecker core needs a constant Jacobian per cell
     v = "" if version == 1 else str(version)
     return hasattr(lib, f"bdx_fused{v}_apply_{pb.suf}_p{pb.degree}")
 
@@ -40,7 +42,8 @@ def fused_supported(pb, version: int = 1) -> bool:
 class FusedLaplacianGPU:
     """version=1: lap_fused.h (OTF or stored G); version=2: lap_fused2.h
     (OTF only, precomputed per-thread addressing); version=3: lap_fused3.h
-    (fused2 + direct-gradient contraction core, phi0 != I only)."""
+    (fused2 + direct-gradient contraction core, phi0 != I only); version=4:
+    lap_fused4.h (MFMA Kronecker core for parallelepiped cells, FP64 Q3)."""
 
     def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True,
                  runtime: str = "native"):
@@ -58,6 +61,8 @@ class FusedLaplacianGPU:
         # fused2: constant-Jacobian kernel instance when every local cell is a
         # parallelepiped (bitwise edge check on the host); else the trilinear one
         self.affine = bool(affine and pb.all_affine)
+        if version == 4 and not self.affine:
+            raise ValueError("fused4 needs parallelepiped cells (constant Jacobian)")
         if version >= 2:
             geometry = "otf-affine" if self.affine else "otf-general"
         self.name = "fused" if version == 1 else f"fused{version}"
@@ -68,7 +73,11 @@ class FusedLaplacianGPU:
         t = pb.kernels.t
         self.t = t
         ty, tz = ctypes.c_int(0), ctypes.c_int(0)
-        _check(self.lib.bdx_fused_tile(t.nq, ctypes.byref(ty), ctypes.byref(tz)), "fused_tile")
+        if version == 4:
+            _check(self.lib.bdx_fused4_tile(ctypes.byref(ty), ctypes.byref(tz)), "fused4_tile")
+        else:
+            _check(self.lib.bdx_fused_tile(t.nq, ctypes.byref(ty), ctypes.byref(tz)),
+                   "fused_tile")
         self.TY, self.TZ = ty.value, tz.value
         P = lat.degree
         self.nty = max(1, math.ceil(lat.n[1] / self.TY))
@@ -87,18 +96,29 @@ class FusedLaplacianGPU:
                 self.G = torch.empty(lat.ncells_local * 6 * t.nq ** 3, dtype=dt, device=dev)
                 pb.kernels.geometry(pb.xv, self.G)
         # packed 1D tables (uniform rows are read through scalar loads)
-        if version == 3:
+        if version == 4:
+            # 1D mass / stiffness / mixed matrices of the quadrature rule
             self._Dd = np.ascontiguousarray(pb.tables.Dd, dtype=np.float64)
-            ftab = getattr(self.lib, f"bdx_fused3_tables_{pb.suf}")
-            second = self._Dd
+            ftab4 = getattr(self.lib, f"bdx_fused4_tables_{pb.suf}")
+            wts = np.ascontiguousarray(t.wts, dtype=np.float64)
+            ntab = ftab4(t.nd, t.nq, ptr(t.phi0), ptr(self._Dd), ptr(wts), None)
+            if ntab <= 0:
+                raise RuntimeError(f"no fused4 tables for nd={t.nd} nq={t.nq}")
+            host = np.zeros(ntab, dtype=np.float64)
+            ftab4(t.nd, t.nq, ptr(t.phi0), ptr(self._Dd), ptr(wts), ptr(host))
         else:
-            ftab = getattr(self.lib, f"bdx_fused_tables_{pb.suf}")
-            second = t.dphi1
-        ntab = ftab(t.nd, t.nq, ptr(t.phi0), ptr(second), None)
-        if ntab <= 0:
-            raise RuntimeError(f"no fused tables for nd={t.nd} nq={t.nq}")
-        host = np.zeros(ntab, dtype=np.float64 if pb.dtype == torch.float64 else np.float32)
-        ftab(t.nd, t.nq, ptr(t.phi0), ptr(second), ptr(host))
+            if version == 3:
+                self._Dd = np.ascontiguousarray(pb.tables.Dd, dtype=np.float64)
+                ftab = getattr(self.lib, f"bdx_fused3_tables_{pb.suf}")
+                second = self._Dd
+            else:
+                ftab = getattr(self.lib, f"bdx_fused_tables_{pb.suf}")
+                second = t.dphi1
+            ntab = ftab(t.nd, t.nq, ptr(t.phi0), ptr(second), None)
+            if ntab <= 0:
+                raise RuntimeError(f"no fused tables for nd={t.nd} nq={t.nq}")
+            host = np.zeros(ntab, dtype=np.float64 if pb.dtype == torch.float64 else np.float32)
+            ftab(t.nd, t.nq, ptr(t.phi0), ptr(second), ptr(host))
         self.tabs = host  # host memory: copied into the kernel arguments
         if version >= 2:
             self._apply2 = getattr(self.lib, f"bdx_fused{version}_apply_{pb.suf}_p{P}")

@@ -37,7 +37,7 @@ def declare(lib) -> None:
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                vp, vp, vp, vp, f64, vp, vp, i32, i32, i32, i32, vp])
-        for P, v in [(P, v) for P in range(1, 8) for v in (2, 3)]:
+        for P, v in [(P, v) for P in range(1, 8) for v in (2, 3, 4)]:
             name = f"bdx_fused{v}_apply_{suf}_p{P}"
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -48,7 +48,11 @@ def declare(lib) -> None:
         _d(lib, f"bdx_xflush_{suf}", [vp, vp, vp, vp, vp, i32, i32, vp])
         _d(lib, f"bdx_fused_tables_{suf}", [i32, i32, vp, vp, vp])
         _d(lib, f"bdx_fused3_tables_{suf}", [i32, i32, vp, vp, vp])
+        if hasattr(lib, f"bdx_fused4_tables_{suf}"):
+            _d(lib, f"bdx_fused4_tables_{suf}", [i32, i32, vp, vp, vp, vp])
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
+    if hasattr(lib, "bdx_fused4_tile"):
+        _d(lib, "bdx_fused4_tile", [vp, vp])
     # native CG runtime (runtime.hip)
     _d(lib, "bdx_rt_nccl_unique_id", [vp])
     _d(lib, "bdx_rt_create", [i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,

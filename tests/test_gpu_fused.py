@@ -31,6 +31,8 @@ CASES = [
     ((3, 3, 8), 5, 1, False, 0.2, torch.float64),
     ((5, 4, 7), 3, 1, False, 0.2, torch.float32),
     ((2, 3, 3), 6, 1, False, 0.1, torch.float32),
+    ((6, 9, 11), 3, 1, False, 0.0, torch.float64),
+    ((5, 8, 13), 3, 1, True, 0.0, torch.float64),
 ]
 
 
@@ -40,13 +42,13 @@ def _tol(dt):
 
 # (geometry, kernel version, affine fast path allowed)
 VARIANTS = [("otf", 1, True), ("stored", 1, True), ("otf", 2, True), ("otf", 2, False),
-            ("otf", 3, True), ("otf", 3, False)]
+            ("otf", 3, True), ("otf", 3, False), ("otf", 4, True)]
 
 
 def _skip_unsupported(pb, version):
     from benchmark_dolfinx_amd.models.fused import fused_supported
     if not fused_supported(pb, version):
-        pytest.skip(f"fused{version} does not cover this element (phi0 == I)")
+        pytest.skip(f"fused{version} does not cover this element / mesh / dtype")
 
 
 @pytest.mark.parametrize("geometry,version,affine", VARIANTS)
@@ -76,6 +78,7 @@ def test_fused_cg_matches_host_cg(geometry, version, affine, pert, runtime):
         pytest.skip("the native runtime drives fused2/3")
     nc = (5, 7, 11)
     gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", pert)
+    _skip_unsupported(gpu, version)
     cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", pert)
     xg = gpu.new_vector()
     DeviceCG(gpu).solve(FusedLaplacianGPU(gpu, geometry, version, affine, runtime), xg,
@@ -100,9 +103,11 @@ def _cg_job(comm, nc, P, nreps, geometry, version=1, pert=0.1, runtime="native")
 
 @pytest.mark.parametrize("runtime", ["native", "python"])
 @pytest.mark.parametrize("pert", [0.0, 0.1])
-@pytest.mark.parametrize("version", [1, 2, 3])
+@pytest.mark.parametrize("version", [1, 2, 3, 4])
 @pytest.mark.parametrize("ranks", [2, 4, 8])
 def test_fused_partition_invariance_threaded(ranks, version, pert, runtime):
+    if version == 4 and pert:
+        pytest.skip("fused4 needs parallelepiped cells")
     if version == 1 and runtime == "native":
         pytest.skip("the native runtime drives fused2/3")
     ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert, runtime)[0]
@@ -112,9 +117,9 @@ def test_fused_partition_invariance_threaded(ranks, version, pert, runtime):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
 
 
-@pytest.mark.parametrize("version", [1, 2, 3])
+@pytest.mark.parametrize("version", [1, 2, 3, 4])
 def test_fused_golden_and_mat_comp_16(version):
-    if version < 3:  # qmode=0 (phi0 == I) is not a fused3 element
+    if version != 3:  # qmode=0 (phi0 == I) is not a fused3 element
         nx = compute_mesh_size(1000, 3)
         pb = PoissonProblem(Comm(), nx, 3, 0, False, torch.float64, "gpu")
         u = pb.assemble_rhs()
@@ -144,12 +149,15 @@ def test_fused3_cg_all_degrees(P, nc, pert):
     assert rel < 1e-10, rel
 
 
-@pytest.mark.parametrize("kernel", ["fused3", "fused2", "v1"])
-@pytest.mark.parametrize("nc,P,pert", [((4, 5, 7), 3, 0.0), ((3, 4, 5), 6, 0.1), ((5, 6, 6), 2, 0.0)])
+@pytest.mark.parametrize("kernel", ["fused4", "fused3", "fused2", "v1"])
+@pytest.mark.parametrize("nc,P,pert", [((4, 5, 7), 3, 0.0), ((3, 4, 5), 6, 0.1), ((5, 6, 6), 2, 0.0),
+                                       ((9, 13, 10), 3, 0.0)])
 def test_random_coefficients_gpu(kernel, nc, P, pert):
     """Per-cell random kappa: GPU kernels vs the C++ CPU operator, and CG."""
     from benchmark_dolfinx_amd.driver import make_operator
     gpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "gpu", pert, "random")
+    if kernel == "fused4" and not (P == 3 and pert == 0.0):
+        pytest.skip("fused4: Q3 parallelepiped cells")
     cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", pert, "random")
     rng = np.random.default_rng(5)
     u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
