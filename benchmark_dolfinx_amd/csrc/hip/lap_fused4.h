@@ -35,6 +35,15 @@
 #ifndef BDX_F4_WAVES
 #define BDX_F4_WAVES 2
 #endif
+// Timing-only phase drops for A/B attribution (wrong numerics when nonzero):
+// 1 = MFMA core, 2 = gather + write-out, 4 = next-layer global loads,
+// 8 = x contraction + geometry.
+#ifndef BDX_F4_NOSKIP
+#define BDX_F4_NOSKIP 0
+#endif
+#ifndef BDX_F4_DROP
+#define BDX_F4_DROP 0
+#endif
 
 typedef double bdx_f64x4 __attribute__((ext_vector_type(4)));
 typedef double bdx_f64x2 __attribute__((ext_vector_type(2)));
@@ -289,7 +298,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
-      if (!last && (st_meta[k] & kValid)) {
+      if (!(BDX_F4_DROP & 4) && !last && (st_meta[k] & kValid)) {
         pf_r[k] = A.u[lnext + st_goff[k]];
         if constexpr (MODE == kFusedCG) {
           pf_p[k] = A.pold[lnext + st_goff[k]];
@@ -308,7 +317,14 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
 
     // ------------------------------------------------ geometry (constant J)
     T G00, G01, G02, G11, G12, G22;
-    {
+    if constexpr ((BDX_F4_DROP & 8) != 0) {
+      G00 = sX[c];
+      G01 = sX[c + 1];
+      G02 = sX[c + 2];
+      G11 = sX[c + 3];
+      G12 = sX[c + 4];
+      G22 = sX[c + 5];
+    } else {
       const T* X0 = sX;
       const T* X1 = sX + NV;
       const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
@@ -351,6 +367,11 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       for (int j = 0; j < ND; ++j) uu[l][j] = ub[l * PLP + j * DZP];
     bdx_f64x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
     auto block = [&](int t, const T (&V)[ND], T gt) {
+      if constexpr ((BDX_F4_DROP & 1) != 0) {
+        acc0[t & 3] += V[0] + V[1];
+        acc1[t & 3] += V[2] + V[3] + gt;
+        return;
+      }
       const bdx_f64x2 a01 = *reinterpret_cast<const bdx_f64x2*>(s_Al + (2 * t) * 128);
       const bdx_f64x2 a23 = *reinterpret_cast<const bdx_f64x2*>(s_Al + (2 * t + 1) * 128);
       acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a01[0], gt * V[0], acc0, 0, 0, 0);
@@ -359,6 +380,11 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a23[1], gt * V[3], acc1, 0, 0, 0);
     };
     auto xcontract = [&](int m, T (&V)[ND]) {
+      if constexpr ((BDX_F4_DROP & 8) != 0) {
+#pragma unroll
+        for (int j = 0; j < ND; ++j) V[j] = uu[m][j];
+        return;
+      }
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
         T s = T(0);
@@ -368,19 +394,31 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       }
     };
     {
+      // Cells whose Jacobian is diagonal (axis-aligned boxes) have
+      // G01 = G02 = G12 = 0 exactly; when that holds for every cell of the
+      // wave the five mixed blocks contribute exact zeros to the MFMA
+      // accumulators and are skipped (wave-uniform branch, bit-identical
+      // result).  BDX_F4_NOSKIP=1 always runs them (A/B and documentation).
+#if BDX_F4_NOSKIP
+      const bool mixed = true;
+#else
+      const bool mixed = __any((G01 != T(0)) || (G02 != T(0)) || (G12 != T(0)));
+#endif
       T V[ND];
       xcontract(1, V);  // K1 along x
       block(0, V, G00);
-      xcontract(2, V);  // C1
-      block(4, V, G01);
-      block(6, V, G02);
-      xcontract(3, V);  // C1^T
-      block(5, V, G01);
-      block(7, V, G02);
+      if (mixed) {
+        xcontract(2, V);  // C1
+        block(4, V, G01);
+        block(6, V, G02);
+        xcontract(3, V);  // C1^T
+        block(5, V, G01);
+        block(7, V, G02);
+      }
       xcontract(0, V);  // M1
       block(1, V, G11);
       block(2, V, G22);
-      block(3, V, G12);
+      if (mixed) block(3, V, G12);
     }
     const bdx_f64x4 ye = acc0 + acc1;
     // lane holds y_e[cell][x = xi][y = r][z = g], r = 0..3
@@ -399,7 +437,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     __syncthreads();
 
     // ------------------------------------------------ gather-sum and write out
-    {
+    if constexpr ((BDX_F4_DROP & 2) == 0) {
       const int64_t lbase = static_cast<int64_t>(cx) * P;
       T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
                                   A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};

@@ -274,13 +274,19 @@ def make_local_lattice(rank: int, nranks: int, ncells: tuple[int, int, int],
 
 
 def vertex_coordinates(lat: LocalLattice, perturb: float = 0.0,
-                       seed: int = 42) -> np.ndarray:
+                       seed: int = 42, shear: float = 0.0) -> np.ndarray:
     """Local vertex lattice coordinates, shape (nx+1, ny+1, nz+1, 3).
 
     With ``perturb != 0`` the x coordinate of every vertex (boundary vertices
     included, like `src/mesh.cpp:199-207`) moves by U(-perturb/nx, perturb/nx).
     The random value is a counter-based hash of the *global* vertex id, so the
     mesh is identical for every partition (fixes reference quirk Q11).
+
+    ``shear != 0`` applies the global linear map (x, y, z) -> (x + s y,
+    y + s z, z + s x): every cell stays a parallelepiped but its Jacobian is
+    full (all geometry factors nonzero).  Test-only; with power-of-two cell
+    counts and a dyadic s the map is exact in floating point, so the
+    bitwise parallelepiped check still holds.
     """
     nxg, nyg, nzg = lat.ncells_global
     vx = np.arange(lat.c0[0], lat.c1[0] + 1, dtype=np.float64)
@@ -299,6 +305,11 @@ def vertex_coordinates(lat: LocalLattice, perturb: float = 0.0,
         u = _hash_uniform(gid, seed)
         amp = perturb / nxg
         X[..., 0] += (2.0 * u - 1.0) * amp
+    if shear != 0.0:
+        x0, y0, z0 = X[..., 0].copy(), X[..., 1].copy(), X[..., 2].copy()
+        X[..., 0] = x0 + shear * y0
+        X[..., 1] = y0 + shear * z0
+        X[..., 2] = z0 + shear * x0
     return X
 
 

@@ -60,7 +60,7 @@ def cells_all_parallelepipeds(X: np.ndarray) -> bool:
 class PoissonProblem:
     def __init__(self, comm: Comm, ncells, degree: int, qmode: int = 1,
                  use_gauss: bool = False, dtype=torch.float64, platform: str = "gpu",
-                 perturb: float = 0.0, coefficient: str = "constant"):
+                 perturb: float = 0.0, coefficient: str = "constant", shear: float = 0.0):
         if use_gauss and qmode == 0:
             # same validation as the reference (src/laplacian.hpp:197-198, Q5)
             raise RuntimeError("Expecting identity matrix for qmode=0")
@@ -77,7 +77,7 @@ class PoissonProblem:
         self.lat: LocalLattice = make_local_lattice(comm.rank, comm.size, tuple(ncells), degree)
         npdt = _np_dtype(dtype)
         with timed("~setup mesh"):
-            xv = vertex_coordinates(self.lat, perturb).astype(npdt)
+            xv = vertex_coordinates(self.lat, perturb, shear=shear).astype(npdt)
             self.xv_host = np.ascontiguousarray(xv)
             self.xv = torch.from_numpy(self.xv_host).to(self.device)
         self.host_tables = {k: np.ascontiguousarray(v, dtype=npdt) for k, v in dict(

@@ -175,3 +175,55 @@ def test_random_coefficients_gpu(kernel, nc, P, pert):
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 10)
     rel = (o(xg.cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
     assert rel < 1e-10, rel
+
+
+@pytest.mark.parametrize("nc,coef", [((4, 8, 8), "constant"), ((8, 4, 16), "random"),
+                                     ((16, 8, 4), "constant")])
+@pytest.mark.parametrize("shear", [0.5, 0.25])
+def test_fused4_sheared_parallelepipeds(nc, coef, shear):
+    """fused4's mixed Kronecker blocks (G01/G02/G12 != 0): sheared mesh whose
+    cells are parallelepipeds with a full Jacobian; action vs the C++ CPU
+    operator and CG vs the host CG."""
+    from benchmark_dolfinx_amd.models.fused import fused_supported
+    gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", 0.0, coef, shear)
+    cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", 0.0, coef, shear)
+    assert gpu.all_affine and fused_supported(gpu, 4)
+    rng = np.random.default_rng(11)
+    u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
+    yc = cpu.new_vector()
+    MatFreeLaplacianCPU(cpu).apply(u64, yc)
+    op = FusedLaplacianGPU(gpu, "otf", 4)
+    yg = gpu.new_vector()
+    op.apply(u64.to(gpu.device), yg)
+    o = cpu.owned
+    err = (o(yg.cpu()) - o(yc)).abs().max().item()
+    assert err <= 1e-12 * 50 * yc.abs().max().item(), err
+    xg = gpu.new_vector()
+    DeviceCG(gpu).solve(op, xg, gpu.assemble_rhs(), 20)
+    xc = cpu.new_vector()
+    cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 20)
+    rel = (o(xg.cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
+    assert rel < 1e-10, rel
+    op.close()
+
+
+def _cg_job_shear(comm, nc, nreps):
+    pb = PoissonProblem(comm, nc, 3, 1, False, torch.float64, "gpu", 0.0, "random", 0.5)
+    u = pb.assemble_rhs()
+    x = pb.new_vector()
+    op = FusedLaplacianGPU(pb, "otf", 4)
+    DeviceCG(pb).solve(op, x, u, nreps)
+    y = pb.new_vector()
+    op.apply(u, y)
+    torch.cuda.synchronize()
+    op.close()
+    return pb.norm(u), pb.norm(x), pb.norm(y)
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_fused4_sheared_partition_invariance(ranks):
+    ref = run_threaded(1, _cg_job_shear, (8, 8, 16), 12)[0]
+    got = run_threaded(ranks, _cg_job_shear, (8, 8, 16), 12)
+    for r in got:
+        for a, b in zip(r, ref):
+            assert abs(a - b) <= 1e-11 * abs(b), (r, ref)

@@ -142,3 +142,19 @@ def test_parallelepiped_detection():
     Xb = X.copy()
     Xb[2, 2, 1, 1] += 1e-9
     assert not cells_all_parallelepipeds(Xb)
+
+
+def test_sheared_mesh_is_parallelepiped_with_full_jacobian():
+    """The test-only shear map keeps every cell a parallelepiped (bitwise
+    check, needed by the fused4 kernel) while making the Jacobian full, so
+    the mixed geometry terms G01/G02/G12 are exercised."""
+    import torch
+    from benchmark_dolfinx_amd.models.poisson import PoissonProblem
+    from benchmark_dolfinx_amd.parallel.comm import Comm
+    pb = PoissonProblem(Comm(), (4, 8, 8), 3, 1, False, torch.float64, "cpu", 0.0,
+                        "constant", 0.5)
+    assert pb.all_affine
+    X = pb.xv_host
+    J = np.stack([X[1, 0, 0] - X[0, 0, 0], X[0, 1, 0] - X[0, 0, 0], X[0, 0, 1] - X[0, 0, 0]], 1)
+    off = J - np.diag(np.diag(J))
+    assert np.all(np.abs(off[np.nonzero(off)]) > 0) and np.count_nonzero(off) == 3
