@@ -44,7 +44,11 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         elif geometry == "otf-general" or not pb.all_affine:
             kernel = "fused2"
         else:
-            kernel = os.environ.get("BDX_AUTO_AFFINE", "fused3")
+            # fused4 (MFMA Kronecker core) where an instance exists: Q3 FP64
+            # 7.57 ms/iteration vs fused3 12.0 ms (profiles/r1_q3_fused4_stats.md)
+            from .models.fused import fused_supported
+            kernel = os.environ.get("BDX_AUTO_AFFINE",
+                                    "fused4" if fused_supported(pb, 4) else "fused3")
     if kernel == "fused4":
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 4) and geometry in ("auto", "otf"):
