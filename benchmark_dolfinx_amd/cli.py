@@ -54,7 +54,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="Use Gauss quadrature rather than GLL quadrature")
     ap.add_argument("--json", default="", help="Filename for JSON output")
     # MI355X extensions
-    ap.add_argument("--kernel", default="auto", choices=["auto", "fused4", "fused3", "fused2", "fused", "v1"],
+    ap.add_argument("--kernel", default="auto", choices=["auto", "fused5", "fused4", "fused3", "fused2", "fused", "v1"],
                     help="GPU operator kernel: fused structured kernel or the generic v1")
     ap.add_argument("--geometry", default="auto", choices=["auto", "otf", "otf-general", "stored"],
                     help="Geometry factors on the fly (otf: constant-Jacobian fast path for "

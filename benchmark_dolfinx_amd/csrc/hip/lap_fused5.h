@@ -1,0 +1,708 @@
+// Fused structured operator kernel, v5 ("fused5"): nodal Kronecker sum
+// factorisation for parallelepiped cells, any degree P = 3..7, FP64 / FP32.
+//
+// For a cell with a constant Jacobian the quadrature sum of the reference
+// stiffness operator (src/laplacian_gpu.hpp:91-426 with
+// src/geometry_gpu.hpp:26-132) factorises exactly into 1D matrices of the
+// same quadrature rule (see lap_fused4.h):
+//   M = B^T W B,  K = Dd^T W Dd,  C = Dd^T W B   (B = phi0, Dd = dphi1 phi0),
+//   A_e = G00 K.M.M + G11 M.K.M + G22 M.M.K + G12 M.(C.Ct + Ct.C)
+//       + G01 (C.Ct.M + Ct.C.M) + G02 (C.M.Ct + Ct.M.C)      (x . y . z).
+// fused4 contracts the (y, z) factor as one 16 x 16 MFMA operand, which only
+// pays at ND = 4.  Here the three directions are applied one after another
+// on ND x ND nodal matrices -- no quadrature-point arrays at all (ND^3 instead
+// of NQ^3 values per cell, 343 vs 512 at Q6) -- with every pass reading its
+// input line once:
+//   x pass   lane (j, k) holds the x-line u[.][j][k] (slab LDS -> registers),
+//            forms Kx u, Mx u (+ Cx u, Ct_x u on sheared cells);
+//   z pass   lane (i, j) reads its z-lines (one 16-byte vector row each) and
+//            forms the y-factor groups
+//              zM  = G00 Mz(Kx u) + G22 Kz(Mx u) [+ G02 (Ctz(Cx u) + Cz(Ctx u))]
+//              zK  = G11 Mz(Mx u)
+//             [zCt = G01 Mz(Cx u) + G12 Cz(Mx u)]
+//             [zC  = G01 Mz(Ctx u) + G12 Ctz(Mx u)];
+//   y pass   lane (i, k) reads its y-lines and forms
+//              y_e = My zM + Ky zK [+ Ct_y zCt + C_y zC].
+// A cell is one wave for ND >= 6 (ND^2 lanes of 64) and 2 / 4 cells share a
+// wave at ND = 5 / 4, so the passes exchange data only inside a wave:
+// wave-local syncs, in-place rewrites of one per-wave buffer, two workgroup
+// barriers per cell layer (gather and staging).  The 1D matrices are
+// wave-uniform kernarg values (scalar loads).  On axis-aligned boxes
+// (diagonal Jacobians, the benchmark mesh; exact host check) the 2-array
+// instance runs: 7 ND^2 FMAs per lane and cell.
+//
+// Everything around the core -- the x-march over (y, z) tiles, the double
+// buffered slab staging with the CG fusion (p = r + beta p_old, lagged
+// x update, Dirichlet identity rows, p.Ap partials as element dots) and the
+// atomic-free gather with tile-interface buffers -- is fused4's.
+#pragma once
+#include <cstring>
+#include <mutex>
+
+#include "lap_fused2.h"
+
+#ifndef BDX_F5_WAVES
+#define BDX_F5_WAVES 2
+#endif
+// Timing-only phase drops for A/B attribution (wrong numerics when nonzero):
+// 1 = z/y passes, 2 = gather + write-out, 4 = next-layer global loads.
+#ifndef BDX_F5_DROP
+#define BDX_F5_DROP 0
+#endif
+
+// kernarg table layout: M, K, C, C^T as 8 x 8 row-major blocks
+constexpr int kF5Stride = 8;
+constexpr int kF5Tab = 4 * 64;
+static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
+
+template <int ND> struct F5Tile;  // cells per wave and (y, z) tile per degree
+template <> struct F5Tile<4> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
+template <> struct F5Tile<5> { static constexpr int CPW = 2, TY = 2, TZ = 4; };
+template <> struct F5Tile<6> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+#ifndef BDX_F5_TY7
+#define BDX_F5_TY7 2
+#endif
+#ifndef BDX_F5_TZ7
+#define BDX_F5_TZ7 2
+#endif
+template <> struct F5Tile<7> { static constexpr int CPW = 1, TY = BDX_F5_TY7, TZ = BDX_F5_TZ7; };
+template <> struct F5Tile<8> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+
+template <typename T, int ND, int NARR>
+struct F5Shape {
+  static constexpr int P = ND - 1;
+  static constexpr int CPW = F5Tile<ND>::CPW, TY = F5Tile<ND>::TY, TZ = F5Tile<ND>::TZ;
+  static constexpr int CELLS = TY * TZ;
+  static_assert(CELLS % CPW == 0, "whole waves of cells");
+  static constexpr int WAVES = CELLS / CPW;
+  static constexpr int NT = WAVES * 64;
+  static constexpr int VW = VecOf<T>::W;
+  // line pitch: an odd number of 16-byte slots (conflict-free b128 rows)
+  static constexpr int SLOTS = (ND + VW - 1) / VW;
+  static constexpr int NDP = (SLOTS % 2 ? SLOTS : SLOTS + 1) * VW;
+  static constexpr int ARR = CPW * ND * ND * NDP;  // one array of line rows
+  // element vectors for the gather: E[cell][j][k][i]
+  static constexpr int RP = ND, P1 = ND * ND, PC = ND * ND * ND;
+  static constexpr int WB0 = NARR * ARR;
+  static constexpr int WB = WB0 > CPW * PC ? WB0 : CPW * PC;  // per-wave buffer
+  static constexpr int DY = TY * P + 1, DZ = TZ * P + 1, PL = DY * DZ;
+  static constexpr int DZP = DZ | 1, PLP = DY * DZP;
+};
+
+template <typename T, int ND, int NARR, int MODE>
+__global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
+    lap_fused5_kernel(Fused2Args<T> A, const T* __restrict__ tabd) {
+  using S = F5Shape<T, ND, NARR>;
+  constexpr int P = S::P, CPW = S::CPW, TY = S::TY, TZ = S::TZ;
+  constexpr int DY = S::DY, DZ = S::DZ, PL = S::PL, DZP = S::DZP, PLP = S::PLP;
+  constexpr int NT = S::NT, ND2 = ND * ND, NDP = S::NDP, ARR = S::ARR, WB = S::WB;
+  constexpr int RP = S::RP, P1 = S::P1, PC = S::PC;
+  constexpr bool MIXED = NARR == 4;
+  constexpr int NPF = (P * PL + NT - 1) / NT;
+  constexpr int NOUT = (ND * PL + NT - 1) / NT;
+  constexpr int NCP = (PL + NT - 1) / NT;
+  constexpr int NV = (TY + 1) * (TZ + 1) * 3;
+  constexpr int NPV = (NV + NT - 1) / NT;
+  constexpr int ZSLOT = S::WAVES * WB;
+  static_assert(ZSLOT < 32768, "16-bit LDS source offsets");
+  static_assert(PL < (1 << 19), "plane index field");
+  static_assert(ND * PLP < (1 << 23), "staging offset field");
+
+  __shared__ __attribute__((aligned(16))) T s_w[ZSLOT + 1];
+  __shared__ T s_u[2][ND * PLP];
+  __shared__ T s_c[2][PL];
+  __shared__ T s_X[2][2 * NV];
+  __shared__ double s_red[16];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_w[ZSLOT] = T(0);
+
+  // XCD-aware bijective remap of the block id (cdna_hip_programming.md T1).
+  const int nblk = gridDim.x, ob = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
+  const int ty = bid / A.ntz, tz = bid % A.ntz;
+  const int y0 = ty * TY * P, z0 = tz * TZ * P;
+  const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
+  const int ncx = A.ncx;
+  const bool top_y = (ty == A.nty - 1), top_z = (tz == A.ntz - 1);
+  const int ey = (y0 + DY <= Ly) ? DY : Ly - y0;
+  const int ez = (z0 + DZ <= Lz) ? DZ : Lz - z0;
+  const int oy = top_y ? ey : TY * P;
+  const int oz = top_z ? ez : TZ * P;
+
+  // lane roles: (cell of the wave, a, b); pass-dependent meaning of (a, b)
+  const bool lane_on = lane < CPW * ND2;
+  const int cw = lane_on ? lane / ND2 : 0;
+  const int ab = lane_on ? lane % ND2 : 0;
+  const int la = ab / ND, lb = ab % ND;
+  const int c = wv * CPW + cw;
+  const int cy = c / TZ, cz = c % TZ;
+  const bool cell_on = lane_on && (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
+  T* const Wb = s_w + wv * WB;             // this wave's buffer
+  T* const Wc = Wb + cw * ND2 * NDP;       // this cell's rows of array 0
+
+  T beta = T(0), xalpha = T(0);
+  const bool xupd = MODE == kFusedCG && A.xa_num >= 0;
+  if constexpr (MODE == kFusedCG) {
+    if (A.beta_num >= 0) beta = static_cast<T>(A.scal[A.beta_num] / A.scal[A.beta_den]);
+    if (xupd) xalpha = static_cast<T>(A.scal[A.xa_num] / A.scal[A.xa_den]);
+  }
+  double pap = 0.0;
+
+  enum { kValid = 1, kOwnT = 2, kBcYZ = 4, kRownYZ = 8 };
+  auto yz_flags = [&](int ly, int lz) -> int {
+    if (ly >= ey || lz >= ez) return 0;
+    const int gy = y0 + ly, gz = z0 + lz;
+    int f = kValid;
+    if (ly < oy && lz < oz) f |= kOwnT;
+    if (gy == A.bcy_lo || gy == A.bcy_hi || gz == A.bcz_lo || gz == A.bcz_hi) f |= kBcYZ;
+    if (gy < A.owny && gz < A.ownz) f |= kRownYZ;
+    return f;
+  };
+  auto stage = [&](int f, int gx, const T* __restrict__ ul, T* __restrict__ pn, T* __restrict__ yl,
+                   int goff) -> T {
+    T v;
+    if constexpr (MODE == kFusedCG) {
+      const T po = A.pold[(ul - A.u) + goff];
+      v = ul[goff] + beta * po;
+      if (xupd && (f & kOwnT)) {
+        T* __restrict__ xl = A.x + (ul - A.u);
+        xl[goff] += xalpha * po;
+      }
+      if (f & kOwnT) pn[goff] = v;
+    } else {
+      v = ul[goff];
+    }
+    (void)pn;
+    if ((f & kBcYZ) || gx == A.bcx_lo || gx == A.bcx_hi) {
+      if (f & kOwnT) {
+        const bool rown = (f & kRownYZ) && gx < A.ownx;
+        yl[goff] = rown ? v : T(0);
+        if constexpr (MODE == kFusedCG) {
+          if (rown) pap += static_cast<double>(v) * static_cast<double>(v);
+        }
+      }
+      v = T(0);
+    }
+    return v;
+  };
+
+  // ---- per-thread staging descriptors (planes 1..P of a layer)
+  int st_goff[NPF], st_meta[NPF];
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) {
+    const int e = tid + k * NT;
+    st_goff[k] = 0;
+    st_meta[k] = 0;
+    if (e < P * PL) {
+      const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      const int f = yz_flags(ly, lz);
+      st_goff[k] = (pl * Ly + y0 + ly) * ld + z0 + lz;
+      st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
+    }
+  }
+  // ---- per-thread output descriptors (planes 0..P of a layer)
+  int o_src[NOUT][2], o_off[NOUT], o_meta[NOUT];
+  auto ebase = [&](int cc) { return (cc / CPW) * WB + (cc % CPW) * PC; };
+#pragma unroll
+  for (int k = 0; k < NOUT; ++k) {
+    const int e = tid + k * NT;
+    o_src[k][0] = o_src[k][1] = ZSLOT | (ZSLOT << 16);
+    o_off[k] = 0;
+    o_meta[k] = 0;
+    if (e < ND * PL) {
+      const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      const int f = yz_flags(ly, lz);
+      if (f & kValid) {
+        const int cyh = (ly / P < TY - 1) ? ly / P : TY - 1;
+        const int cyl = (ly % P == 0 && ly > 0 && ly / P - 1 < cyh) ? ly / P - 1 : cyh;
+        const int czh = (lz / P < TZ - 1) ? lz / P : TZ - 1;
+        const int czl = (lz % P == 0 && lz > 0 && lz / P - 1 < czh) ? lz / P - 1 : czh;
+        int src[4] = {ZSLOT, ZSLOT, ZSLOT, ZSLOT};
+        int ns = 0;
+        for (int ccy = cyl; ccy <= cyh; ++ccy)
+          for (int ccz = czl; ccz <= czh; ++ccz)
+            src[ns++] = ebase(ccy * TZ + ccz) + (ly - ccy * P) * P1 + (lz - ccz * P) * RP + pl;
+        o_src[k][0] = src[0] | (src[1] << 16);
+        o_src[k][1] = src[2] | (src[3] << 16);
+        const int gy = y0 + ly, gz = z0 + lz;
+        const bool iy = ly < oy, iz = lz < oz;
+        int kind, off;
+        if (iy && iz) {
+          kind = 0;
+          off = (pl * Ly + gy) * ld + gz;
+        } else if (!iy && iz) {
+          kind = 1;
+          off = static_cast<int>(pl * A.ybps) + ty * Lz + gz;
+        } else if (iy && !iz) {
+          kind = 2;
+          off = static_cast<int>(pl * A.zbps) + gy * (A.ntz - 1) + tz;
+        } else {
+          kind = 3;
+          off = static_cast<int>(pl * A.cbps) + ty * (A.ntz - 1) + tz;
+        }
+        o_off[k] = off;
+        o_meta[k] = f | (kind << 4) | (pl << 8) | (rem << 12);
+      }
+    }
+  }
+  int cp_lds[NCP];
+#pragma unroll
+  for (int k = 0; k < NCP; ++k) {
+    const int e = tid + k * NT;
+    cp_lds[k] = (e < PL) ? (e / DZ) * DZP + e % DZ : -1;
+  }
+  int v_off[NPV];
+#pragma unroll
+  for (int k = 0; k < NPV; ++k) {
+    const int e = tid + k * NT;
+    v_off[k] = -1;
+    if (e < NV) {
+      const int d = e % 3, r = e / 3;
+      const int vz = r % (TZ + 1), vy = r / (TZ + 1);
+      const int gy = ty * TY + vy, gz = tz * TZ + vz;
+      if (gy <= A.n1 && gz <= A.n2) v_off[k] = (gy * (A.n2 + 1) + gz) * 3 + d;
+    }
+  }
+
+  // ---- prologue: layer 0 (planes 0..P), vertex planes 0/1, zero carry
+  for (int e = tid; e < ND * PL; e += NT) {
+    const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+    const int f = yz_flags(ly, lz);
+    T v = T(0);
+    if (f & kValid) v = stage(f, pl, A.u, A.pnew, A.y, (pl * Ly + y0 + ly) * ld + z0 + lz);
+    s_u[0][pl * PLP + ly * DZP + lz] = v;
+  }
+  for (int e = tid; e < 2 * NV; e += NT) {
+    const int k = e % NV;
+    int off = -1;
+    {
+      const int d = k % 3, r = k / 3;
+      const int vz = r % (TZ + 1), vy = r / (TZ + 1);
+      const int gy = ty * TY + vy, gz = tz * TZ + vz;
+      if (gy <= A.n1 && gz <= A.n2) off = (gy * (A.n2 + 1) + gz) * 3 + d;
+    }
+    s_X[0][e] = off >= 0 ? A.xv[(e / NV) * A.vps + off] : T(0);
+  }
+  for (int e = tid; e < PL; e += NT) s_c[0][e] = T(0);
+
+  // wave-local LDS exchange between passes (a wave's lanes run in lockstep)
+  auto wave_sync = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // 1D matrices (kernarg: wave-uniform scalar loads): id 0 = M, 1 = K, 2 = C
+  // The tables (a device copy, see f5_tables_on_device) are read through a
+  // constant-address-space pointer that is laundered per matrix row, so the
+  // scalar loads stream with the FMAs instead of being hoisted out of the
+  // x-march (4 ND^2 doubles would not fit the SGPR file).
+  typedef const __attribute__((address_space(4))) T CT;
+  CT* const tab0 = (CT*)tabd;
+  // out[a] (+)= s * sum_b Mat[a][b] in[b]; id 0 = M, 1 = K, 2 = C, 3 = C^T.
+  // Row a's pointer is laundered through an asm that consumes the result of
+  // row a - 2 (d2): the scalar loads run one row ahead of the FMAs and at
+  // most two rows are live in SGPRs.
+  T d1 = T(0), d2 = T(0);
+  auto matvec = [&](int id, const T (&in)[ND], T (&out)[ND], T s, bool acc) {
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      CT* row = tab0 + id * 64 + a * kF5Stride;
+      asm volatile("" : "+s"(row) : "v"(d2));
+      T t = T(0);
+#pragma unroll
+      for (int b = 0; b < ND; ++b) t += row[b] * in[b];
+      d2 = d1;
+      d1 = t;
+      out[a] = acc ? out[a] + s * t : s * t;
+    }
+  };
+
+  for (int cx = 0; cx < ncx; ++cx) {
+    const int cur = cx & 1, nxt = cur ^ 1;
+    const bool last = (cx == ncx - 1);
+    __syncthreads();
+
+    // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
+    const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
+    T pf_r[NPF], pf_p[NPF], pf_x[NPF];
+    T pf_v[NPV];
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      pf_r[k] = T(0);
+      pf_p[k] = T(0);
+      pf_x[k] = T(0);
+      if (!(BDX_F5_DROP & 4) && !last && (st_meta[k] & kValid)) {
+        pf_r[k] = A.u[lnext + st_goff[k]];
+        if constexpr (MODE == kFusedCG) {
+          pf_p[k] = A.pold[lnext + st_goff[k]];
+          if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = A.x[lnext + st_goff[k]];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPV; ++k) {
+      pf_v[k] = T(0);
+      if (!last && v_off[k] >= 0) pf_v[k] = A.xv[static_cast<int64_t>(cx + 2) * A.vps + v_off[k]];
+    }
+
+    const T* __restrict__ su = s_u[cur];
+    const T* __restrict__ sX = s_X[cur];
+
+    // ------------------------------------------------ geometry (constant J)
+    T G00, G01, G02, G11, G12, G22;
+    {
+      const T* X0 = sX;
+      const T* X1 = sX + NV;
+      const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
+      const int v10 = v00 + (TZ + 1) * 3;
+      T E[3], F[3], Gv[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const T X000 = X0[v00 + d];
+        E[d] = X1[v00 + d] - X000;
+        F[d] = X0[v10 + d] - X000;
+        Gv[d] = X0[v01 + d] - X000;
+      }
+      const T J00 = E[0], J10 = E[1], J20 = E[2];
+      const T J01 = F[0], J11 = F[1], J21 = F[2];
+      const T J02 = Gv[0], J12 = Gv[1], J22 = Gv[2];
+      const T K00 = J11 * J22 - J12 * J21, K01 = J02 * J21 - J01 * J22, K02 = J01 * J12 - J02 * J11;
+      const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
+      const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
+      const T det = J00 * K00 + J01 * K10 + J02 * K20;
+      const T kcell = A.kc ? (cell_on ? A.kc[(static_cast<int64_t>(cx) * A.n1 + ty * TY + cy) * A.n2 +
+                                            tz * TZ + cz]
+                                      : T(0))
+                           : A.kappa;
+      const T sc = cell_on ? kcell * fast_rcp(det) : T(0);
+      G00 = sc * (K00 * K00 + K01 * K01 + K02 * K02);
+      G01 = sc * (K00 * K10 + K01 * K11 + K02 * K12);
+      G02 = sc * (K00 * K20 + K01 * K21 + K02 * K22);
+      G11 = sc * (K10 * K10 + K11 * K11 + K12 * K12);
+      G12 = sc * (K10 * K20 + K11 * K21 + K12 * K22);
+      G22 = sc * (K20 * K20 + K21 * K21 + K22 * K22);
+    }
+    (void)G01;
+    (void)G02;
+    (void)G12;
+
+    // ------------------------------------------------ x pass: lane (j, k) = (la, lb)
+    const T* __restrict__ ucell = su + (cy * P) * DZP + cz * P;
+    {
+      T u[ND];
+#pragma unroll
+      for (int l = 0; l < ND; ++l) u[l] = ucell[l * PLP + la * DZP + lb];
+      T o[ND];
+      // array 0: Kx u, array 1: Mx u [, 2: Cx u, 3: Ctx u]; rows [i][j][k]
+      auto put = [&](int arr) {
+        T* w = Wc + arr * ARR + la * NDP + lb;
+        if (lane_on) {
+#pragma unroll
+          for (int i = 0; i < ND; ++i) w[i * ND * NDP] = o[i];
+        }
+      };
+      matvec(1, u, o, T(1), false);
+      put(0);
+      matvec(0, u, o, T(1), false);
+      put(1);
+      if constexpr (MIXED) {
+        matvec(2, u, o, T(1), false);
+        put(2);
+        matvec(3, u, o, T(1), false);
+        put(3);
+      }
+    }
+    wave_sync();
+
+    // ------------------------------------------------ z pass: lane (i, j) = (la, lb)
+    if constexpr ((BDX_F5_DROP & 1) == 0) {
+      const T* r = Wc + ab * NDP;
+      T ak[ND], am[ND];
+      ldrow<ND>(r, ak);
+      ldrow<ND>(r + ARR, am);
+      T zM[ND], zK[ND];
+      matvec(0, ak, zM, G00, false);
+      matvec(1, am, zM, G22, true);
+      matvec(0, am, zK, G11, false);
+      if constexpr (MIXED) {
+        T ac[ND], at[ND];
+        ldrow<ND>(r + 2 * ARR, ac);
+        ldrow<ND>(r + 3 * ARR, at);
+        T zCt[ND], zC[ND];
+        matvec(3, ac, zM, G02, true);
+        matvec(2, at, zM, G02, true);
+        matvec(0, ac, zCt, G01, false);
+        matvec(2, am, zCt, G12, true);
+        matvec(0, at, zC, G01, false);
+        matvec(3, am, zC, G12, true);
+        wave_sync();
+        // rows [i][k][j]: lane (i, j) writes column j of rows (i, k)
+        if (lane_on) {
+          T* w = Wc + la * ND * NDP + lb;
+#pragma unroll
+          for (int k = 0; k < ND; ++k) {
+            w[2 * ARR + k * NDP] = zCt[k];
+            w[3 * ARR + k * NDP] = zC[k];
+          }
+        }
+      } else {
+        wave_sync();
+      }
+      if (lane_on) {
+        T* w = Wc + la * ND * NDP + lb;
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+          w[k * NDP] = zM[k];
+          w[ARR + k * NDP] = zK[k];
+        }
+      }
+      wave_sync();
+    }
+
+    // ------------------------------------------------ y pass: lane (i, k) = (la, lb)
+    T ye[ND];
+    {
+      const T* r = Wc + ab * NDP;
+      T sM[ND], sK[ND];
+      ldrow<ND>(r, sM);
+      ldrow<ND>(r + ARR, sK);
+      matvec(0, sM, ye, T(1), false);
+      matvec(1, sK, ye, T(1), true);
+      if constexpr (MIXED) {
+        T sCt[ND], sC[ND];
+        ldrow<ND>(r + 2 * ARR, sCt);
+        ldrow<ND>(r + 3 * ARR, sC);
+        matvec(3, sCt, ye, T(1), true);
+        matvec(2, sC, ye, T(1), true);
+      }
+    }
+    // element dot p_e . (A_e p_e): lane holds y_e[i = la][j][k = lb]
+    if constexpr (MODE == kFusedCG) {
+      if (cell_on) {
+#pragma unroll
+        for (int j = 0; j < ND; ++j)
+          pap += static_cast<double>(ucell[la * PLP + j * DZP + lb]) * static_cast<double>(ye[j]);
+      }
+    }
+    wave_sync();
+    if (lane_on) {
+      T* eo = Wb + cw * PC + lb * RP + la;
+#pragma unroll
+      for (int j = 0; j < ND; ++j) eo[j * P1] = cell_on ? ye[j] : T(0);
+    }
+    __syncthreads();
+
+    // ------------------------------------------------ gather-sum and write out
+    if constexpr ((BDX_F5_DROP & 2) == 0) {
+      const int64_t lbase = static_cast<int64_t>(cx) * P;
+      T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
+                                  A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
+#pragma unroll
+      for (int k = 0; k < NOUT; ++k) {
+        const int m = o_meta[k];
+        if (!(m & kValid)) continue;
+        const int pl = (m >> 8) & 15, rem = m >> 12;
+        T v = s_w[o_src[k][0] & 0xffff] + s_w[o_src[k][0] >> 16] +
+              s_w[o_src[k][1] & 0xffff] + s_w[o_src[k][1] >> 16];
+        if (pl == 0) v += s_c[cur][rem];
+        if (pl == P && !last) {
+          s_c[nxt][rem] = v;
+          continue;
+        }
+        const int gxx = cx * P + pl;
+        const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
+        const int kind = (m >> 4) & 3;
+        if (bc) {
+          if (kind == 0) continue;  // Dirichlet y was written at staging
+          v = T(0);
+        }
+        T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
+        dst[o_off[k]] = v;
+      }
+    }
+
+    // ------------------------------------------------ stage the next layer
+    if (!last) {
+      T* __restrict__ un = s_u[nxt];
+#pragma unroll
+      for (int k = 0; k < NCP; ++k)
+        if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
+      T* __restrict__ pnl = A.pnew + lnext;
+      T* __restrict__ yl = A.y + lnext;
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) {
+        const int m = st_meta[k];
+        if (tid + k * NT < P * PL) {
+          T v = T(0);
+          if (m & kValid) {
+            const int gxx = (cx + 1) * P + ((m >> 4) & 15);
+            T val;
+            if constexpr (MODE == kFusedCG) {
+              val = pf_r[k] + beta * pf_p[k];
+            } else {
+              val = pf_r[k];
+            }
+            if constexpr (MODE == kFusedCG) {
+              if (m & kOwnT) {
+                pnl[st_goff[k]] = val;
+                if (xupd) A.x[lnext + st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
+              }
+            }
+            if ((m & kBcYZ) || gxx == A.bcx_hi) {
+              if (m & kOwnT) {
+                const bool rown = (m & kRownYZ) && gxx < A.ownx;
+                yl[st_goff[k]] = rown ? val : T(0);
+                if constexpr (MODE == kFusedCG) {
+                  if (rown) pap += static_cast<double>(val) * static_cast<double>(val);
+                }
+              }
+              val = T(0);
+            }
+            v = val;
+          }
+          un[m >> 8] = v;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NPV; ++k) {
+        const int e = tid + k * NT;
+        if (e < NV) s_X[nxt][e] = sX[NV + e];
+      }
+#pragma unroll
+      for (int k = 0; k < NPV; ++k) {
+        const int e = tid + k * NT;
+        if (e < NV) s_X[nxt][NV + e] = pf_v[k];
+      }
+    }
+  }
+  if constexpr (MODE == kFusedCG) {
+    const double t = block_sum(pap, s_red);
+    if (tid == 0) A.partials[blockIdx.x] = t;
+  }
+}
+
+// 1D matrices of the quadrature rule (host, double, cast to T): M = B^T W B,
+// K = Dd^T W Dd, C = Dd^T W B with B = phi0 (nq x nd), Dd = dphi1 phi0.
+template <typename T>
+inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, const double* wts,
+                        T* out) {
+  if (nd < 2 || nd > kF5Stride || nq < 1 || nq > kMaxNq) return -1;
+  if (!out) return kFusedTabMax;
+  for (int i = 0; i < kFusedTabMax; ++i) out[i] = T(0);
+  for (int i = 0; i < nd; ++i)
+    for (int l = 0; l < nd; ++l) {
+      double m = 0, k = 0, c = 0;
+      for (int q = 0; q < nq; ++q) {
+        m += wts[q] * phi0[q * nd + i] * phi0[q * nd + l];
+        k += wts[q] * Dd[q * nd + i] * Dd[q * nd + l];
+        c += wts[q] * Dd[q * nd + i] * phi0[q * nd + l];
+      }
+      out[i * kF5Stride + l] = static_cast<T>(m);
+      out[64 + i * kF5Stride + l] = static_cast<T>(k);
+      out[128 + i * kF5Stride + l] = static_cast<T>(c);
+      out[192 + l * kF5Stride + i] = static_cast<T>(c);
+    }
+  return kFusedTabMax;
+}
+
+// affine_ok: 0 = general cells (refused), 1 = parallelepipeds, 2 = axis-aligned
+// boxes (diagonal Jacobians: the 2-array instance)
+template <typename T, int ND, int MODE>
+int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStream_t st) {
+  const int nblk = a.nty * a.ntz;
+  if (nblk <= 0) return 0;
+  if (affine_ok == 2)
+    lap_fused5_kernel<T, ND, 2, MODE><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
+  else
+    lap_fused5_kernel<T, ND, 4, MODE><<<nblk, F5Shape<T, ND, 4>::NT, 0, st>>>(a, tabd);
+  return static_cast<int>(hipGetLastError());
+}
+
+// Device copy of the host tables in a per-TU __device__ array: uploaded when
+// the content differs from what the current device holds (a new problem),
+// never inside a stream capture (the first, uncaptured launches of a
+// configuration upload; replays see the same content).  The device is
+// synchronised before an overwrite so no queued kernel reads a half-updated
+// table.  Returns the device address of the array, or null on error.
+template <typename T>
+inline const T* f5_tables_on_device(T* sym_addr_holder, const void* sym, const T* host,
+                                    hipStream_t st, int* err) {
+  static std::mutex mu;
+  static T shadow[16][kFusedTabMax];
+  static bool valid[16] = {};
+  (void)sym_addr_holder;
+  int dev = 0;
+  *err = static_cast<int>(hipGetDevice(&dev));
+  if (*err || dev < 0 || dev >= 16) {
+    if (!*err) *err = static_cast<int>(hipErrorInvalidDevice);
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  if (!valid[dev] || std::memcmp(shadow[dev], host, sizeof(T) * kFusedTabMax) != 0) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if ((*err = static_cast<int>(hipStreamIsCapturing(st, &cs)))) return nullptr;
+    if (cs != hipStreamCaptureStatusNone) {
+      *err = static_cast<int>(hipErrorStreamCaptureUnsupported);
+      return nullptr;
+    }
+    if ((*err = static_cast<int>(hipDeviceSynchronize()))) return nullptr;
+    if ((*err = static_cast<int>(hipMemcpyToSymbol(sym, host, sizeof(T) * kFusedTabMax))))
+      return nullptr;
+    std::memcpy(shadow[dev], host, sizeof(T) * kFusedTabMax);
+    valid[dev] = true;
+  }
+  void* p = nullptr;
+  if ((*err = static_cast<int>(hipGetSymbolAddress(&p, sym)))) return nullptr;
+  return static_cast<const T*>(p);
+}
+
+#define BDX_FUSED5_TU(T, SUF, PP)                                                   \
+  static __device__ T g_f5tab[kFusedTabMax];                                       \
+  extern "C" int bdx_fused5_apply_##SUF##_p##PP(                                   \
+      int mode, int affine_ok, const int64_t* latd, int nq, const double* wts,     \
+      const double* qpts, const T* u, const T* pold, T* pnew, T* x, T* y, T* yb,   \
+      T* zb, T* cb, const T* xv, const T* kc, const T* tabs, double kappa,         \
+      const double* scal, double* partials, int beta_num, int beta_den,            \
+      int xa_num, int xa_den, int nty, int ntz, hipStream_t st) {                  \
+    (void)wts;                                                                     \
+    (void)qpts;                                                                    \
+    (void)nq;                                                                      \
+    if (!affine_ok || !tabs) return static_cast<int>(hipErrorInvalidValue);        \
+    Fused2Args<T> a;                                                               \
+    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));       \
+    a.u = u;                                                                       \
+    a.pold = pold;                                                                 \
+    a.pnew = pnew;                                                                 \
+    a.x = x;                                                                       \
+    a.y = y;                                                                       \
+    a.yb = yb;                                                                     \
+    a.zb = zb;                                                                     \
+    a.cb = cb;                                                                     \
+    a.xv = xv;                                                                     \
+    a.kc = kc;                                                                     \
+    a.scal = scal;                                                                 \
+    a.partials = partials;                                                         \
+    a.beta_num = beta_num;                                                         \
+    a.beta_den = beta_den;                                                         \
+    a.xa_num = xa_num;                                                             \
+    a.xa_den = xa_den;                                                             \
+    a.kappa = static_cast<T>(kappa);                                               \
+    int err = 0;                                                                   \
+    const T* tabd = f5_tables_on_device<T>(nullptr, HIP_SYMBOL(g_f5tab), tabs, st, &err); \
+    if (!tabd) return err ? err : static_cast<int>(hipErrorInvalidValue);          \
+    return mode == kFusedCG ? launch_fused5<T, PP + 1, kFusedCG>(affine_ok, a, tabd, st) \
+                            : launch_fused5<T, PP + 1, kFusedAction>(affine_ok, a, tabd, st); \
+  }                                                                                \
+  extern "C" int bdx_fused5_tables_##SUF##_p##PP(int nd, int nq, const double* phi0, \
+                                                  const double* Dd, const double* wts, \
+                                                  T* out) {                        \
+    return pack_tables5<T>(nd, nq, phi0, Dd, wts, out);                            \
+  }                                                                                \
+  extern "C" int bdx_fused5_tile_p##PP##_##SUF(int* ty, int* tz) {                 \
+    *ty = F5Tile<PP + 1>::TY;                                                      \
+    *tz = F5Tile<PP + 1>::TZ;                                                      \
+    return 0;                                                                      \
+  }

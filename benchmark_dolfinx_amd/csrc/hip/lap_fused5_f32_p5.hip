@@ -1,0 +1,3 @@
+// Fused v5 operator kernels (nodal Kronecker core), float, degree 5.
+#include "lap_fused5.h"
+BDX_FUSED5_TU(float, f32, 5)

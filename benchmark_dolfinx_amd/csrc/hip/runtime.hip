@@ -71,6 +71,11 @@ int bdx_xflush_f32(const int64_t*, const int64_t*, float*, const float*, const d
 BDX_DECL_ALL(2)
 BDX_DECL_ALL(3)
 BDX_DECL_APPLY(4, double, f64, 3)
+#define BDX_DECL_F5(T, SUF) \
+  BDX_DECL_APPLY(5, T, SUF, 3) BDX_DECL_APPLY(5, T, SUF, 4) BDX_DECL_APPLY(5, T, SUF, 5) \
+  BDX_DECL_APPLY(5, T, SUF, 6) BDX_DECL_APPLY(5, T, SUF, 7)
+BDX_DECL_F5(double, f64)
+BDX_DECL_F5(float, f32)
 
 namespace {
 
@@ -87,7 +92,8 @@ ApplyFn<double> apply_fn<double>(int version, int P) {
   if (version == V && P == PP) return bdx_fused##V##_apply_f64_p##PP;
   BDX_CASE(2, 1) BDX_CASE(2, 2) BDX_CASE(2, 3) BDX_CASE(2, 4) BDX_CASE(2, 5) BDX_CASE(2, 6)
   BDX_CASE(2, 7) BDX_CASE(3, 1) BDX_CASE(3, 2) BDX_CASE(3, 3) BDX_CASE(3, 4) BDX_CASE(3, 5)
-  BDX_CASE(3, 6) BDX_CASE(3, 7) BDX_CASE(4, 3)
+  BDX_CASE(3, 6) BDX_CASE(3, 7) BDX_CASE(4, 3) BDX_CASE(5, 3) BDX_CASE(5, 4) BDX_CASE(5, 5)
+  BDX_CASE(5, 6) BDX_CASE(5, 7)
 #undef BDX_CASE
   return nullptr;
 }
@@ -97,7 +103,8 @@ ApplyFn<float> apply_fn<float>(int version, int P) {
   if (version == V && P == PP) return bdx_fused##V##_apply_f32_p##PP;
   BDX_CASE(2, 1) BDX_CASE(2, 2) BDX_CASE(2, 3) BDX_CASE(2, 4) BDX_CASE(2, 5) BDX_CASE(2, 6)
   BDX_CASE(2, 7) BDX_CASE(3, 1) BDX_CASE(3, 2) BDX_CASE(3, 3) BDX_CASE(3, 4) BDX_CASE(3, 5)
-  BDX_CASE(3, 6) BDX_CASE(3, 7)
+  BDX_CASE(3, 6) BDX_CASE(3, 7) BDX_CASE(5, 3) BDX_CASE(5, 4) BDX_CASE(5, 5) BDX_CASE(5, 6)
+  BDX_CASE(5, 7)
 #undef BDX_CASE
   return nullptr;
 }

@@ -44,11 +44,19 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         elif geometry == "otf-general" or not pb.all_affine:
             kernel = "fused2"
         else:
-            # fused4 (MFMA Kronecker core) where an instance exists: Q3 FP64
-            # 7.57 ms/iteration vs fused3 12.0 ms (profiles/r1_q3_fused4_stats.md)
+            # Kronecker cores on parallelepiped meshes (profiles/r1_kernel_ab.md):
+            # fused4 (MFMA) for Q3 FP64 (7.8 ms/iteration vs fused5 8.1, fused3
+            # 12.0), fused5 (nodal sum factorisation) for every other P >= 3
+            # (Q6 FP64 12.1 ms vs fused3 17.8; FP32 8.9 vs 12.4)
             from .models.fused import fused_supported
-            kernel = os.environ.get("BDX_AUTO_AFFINE",
-                                    "fused4" if fused_supported(pb, 4) else "fused3")
+            auto = ("fused4" if fused_supported(pb, 4) else
+                    "fused5" if fused_supported(pb, 5) else "fused3")
+            kernel = os.environ.get("BDX_AUTO_AFFINE", auto)
+    if kernel == "fused5":
+        from .models.fused import FusedLaplacianGPU, fused_supported
+        if fused_supported(pb, 5) and geometry in ("auto", "otf"):
+            return FusedLaplacianGPU(pb, geometry="otf", version=5)
+        kernel = "fused3"
     if kernel == "fused4":
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 4) and geometry in ("auto", "otf"):

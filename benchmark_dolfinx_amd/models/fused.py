@@ -33,8 +33,8 @@ def fused_supported(pb, version: int = 1) -> bool:
     lib = native.hip()
     if version == 3 and pb.tables.is_identity:
         return False  # fused3 is the phi0 != I core
-    if version == 4 and not pb.all_affine:
-        return False  # fused4's Kronecker core needs a constant Jacobian per cell
+    if version in (4, 5) and not pb.all_affine:
+        return False  # the Kronecker cores need a constant Jacobian per cell
     v = "" if version == 1 else str(version)
     return hasattr(lib, f"bdx_fused{v}_apply_{pb.suf}_p{pb.degree}")
 
@@ -43,7 +43,9 @@ class FusedLaplacianGPU:
     """version=1: lap_fused.h (OTF or stored G); version=2: lap_fused2.h
     (OTF only, precomputed per-thread addressing); version=3: lap_fused3.h
     (fused2 + direct-gradient contraction core, phi0 != I only); version=4:
-    lap_fused4.h (MFMA Kronecker core for parallelepiped cells, FP64 Q3)."""
+    lap_fused4.h (MFMA Kronecker core for parallelepiped cells, FP64 Q3);
+    version=5: lap_fused5.h (nodal Kronecker sum factorisation for
+    parallelepiped cells, P = 3..7, FP64 / FP32)."""
 
     def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True,
                  runtime: str = "native"):
@@ -61,8 +63,13 @@ class FusedLaplacianGPU:
         # fused2: constant-Jacobian kernel instance when every local cell is a
         # parallelepiped (bitwise edge check on the host); else the trilinear one
         self.affine = bool(affine and pb.all_affine)
-        if version == 4 and not self.affine:
-            raise ValueError("fused4 needs parallelepiped cells (constant Jacobian)")
+        if version in (4, 5) and not self.affine:
+            raise ValueError(f"fused{version} needs parallelepiped cells (constant Jacobian)")
+        # kernel-instance selector passed as `affine_ok`: fused5 takes 2 on
+        # axis-aligned boxes (diagonal Jacobians: the 2-array instance)
+        self.affine_code = int(self.affine)
+        if version == 5 and pb.all_axis_aligned:
+            self.affine_code = 2
         if version >= 2:
             geometry = "otf-affine" if self.affine else "otf-general"
         self.name = "fused" if version == 1 else f"fused{version}"
@@ -75,6 +82,9 @@ class FusedLaplacianGPU:
         ty, tz = ctypes.c_int(0), ctypes.c_int(0)
         if version == 4:
             _check(self.lib.bdx_fused4_tile(ctypes.byref(ty), ctypes.byref(tz)), "fused4_tile")
+        elif version == 5:
+            _check(getattr(self.lib, f"bdx_fused5_tile_p{pb.degree}_{pb.suf}")(
+                ctypes.byref(ty), ctypes.byref(tz)), "fused5_tile")
         else:
             _check(self.lib.bdx_fused_tile(t.nq, ctypes.byref(ty), ctypes.byref(tz)),
                    "fused_tile")
@@ -96,7 +106,17 @@ class FusedLaplacianGPU:
                 self.G = torch.empty(lat.ncells_local * 6 * t.nq ** 3, dtype=dt, device=dev)
                 pb.kernels.geometry(pb.xv, self.G)
         # packed 1D tables (uniform rows are read through scalar loads)
-        if version == 4:
+        if version == 5:
+            # 1D mass / stiffness / mixed matrices of the quadrature rule, in T
+            self._Dd = np.ascontiguousarray(pb.tables.Dd, dtype=np.float64)
+            ftab5 = getattr(self.lib, f"bdx_fused5_tables_{pb.suf}_p{pb.degree}")
+            wts = np.ascontiguousarray(t.wts, dtype=np.float64)
+            ntab = ftab5(t.nd, t.nq, ptr(t.phi0), ptr(self._Dd), ptr(wts), None)
+            if ntab <= 0:
+                raise RuntimeError(f"no fused5 tables for nd={t.nd} nq={t.nq}")
+            host = np.zeros(ntab, dtype=np.float64 if pb.dtype == torch.float64 else np.float32)
+            ftab5(t.nd, t.nq, ptr(t.phi0), ptr(self._Dd), ptr(wts), ptr(host))
+        elif version == 4:
             # 1D mass / stiffness / mixed matrices of the quadrature rule
             self._Dd = np.ascontiguousarray(pb.tables.Dd, dtype=np.float64)
             ftab4 = getattr(self.lib, f"bdx_fused4_tables_{pb.suf}")
@@ -146,7 +166,7 @@ class FusedLaplacianGPU:
                 xa_num=-1, xa_den=-1, finalize=True):
         pb, t = self.pb, self.t
         if self.version >= 2:
-            _check(self._apply2(mode, int(self.affine), ptr(pb.latd), t.nq, ptr(t.wts),
+            _check(self._apply2(mode, self.affine_code, ptr(pb.latd), t.nq, ptr(t.wts),
                                 ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(x), ptr(y),
                                 ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(pb.xv),
                                 ptr(pb.kc), ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials),

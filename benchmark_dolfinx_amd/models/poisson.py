@@ -37,6 +37,19 @@ def _np_dtype(dtype):
     return np.float64 if dtype == torch.float64 else np.float32
 
 
+def cells_axis_aligned(X: np.ndarray) -> bool:
+    """True iff every cell edge of the vertex lattice X (nx+1, ny+1, nz+1, 3)
+    along lattice axis a has exactly zero components along the other axes:
+    the cells are boxes with diagonal Jacobians, so the geometry factors
+    G01 = G02 = G12 vanish exactly (the fused5 2-array kernel instance)."""
+    for ax in range(3):
+        E = np.diff(X, axis=ax)
+        for d in range(3):
+            if d != ax and E[..., d].size and np.any(E[..., d] != 0):
+                return False
+    return True
+
+
 def cells_all_parallelepipeds(X: np.ndarray) -> bool:
     """True iff every cell of the vertex lattice X (nx+1, ny+1, nz+1, 3) has
     bitwise-equal parallel edges (constant Jacobian).  Evaluated in the
@@ -92,6 +105,7 @@ class PoissonProblem:
         # kept alive for ctypes calls (never pass temporaries to ptr())
         self.latd = self.lat.as_int64()
         self.all_affine = cells_all_parallelepipeds(self.xv_host)
+        self.all_axis_aligned = self.all_affine and cells_axis_aligned(self.xv_host)
         # per-cell kappa (None: the reference's constant kappa = 2)
         self.coefficient = coefficient
         kc = cell_coefficients(self.lat, coefficient, KAPPA)

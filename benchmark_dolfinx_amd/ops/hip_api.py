@@ -37,7 +37,7 @@ def declare(lib) -> None:
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                vp, vp, vp, vp, f64, vp, vp, i32, i32, i32, i32, vp])
-        for P, v in [(P, v) for P in range(1, 8) for v in (2, 3, 4)]:
+        for P, v in [(P, v) for P in range(1, 8) for v in (2, 3, 4, 5)]:
             name = f"bdx_fused{v}_apply_{suf}_p{P}"
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -50,6 +50,10 @@ def declare(lib) -> None:
         _d(lib, f"bdx_fused3_tables_{suf}", [i32, i32, vp, vp, vp])
         if hasattr(lib, f"bdx_fused4_tables_{suf}"):
             _d(lib, f"bdx_fused4_tables_{suf}", [i32, i32, vp, vp, vp, vp])
+        for P in range(1, 8):
+            if hasattr(lib, f"bdx_fused5_tables_{suf}_p{P}"):
+                _d(lib, f"bdx_fused5_tables_{suf}_p{P}", [i32, i32, vp, vp, vp, vp])
+                _d(lib, f"bdx_fused5_tile_p{P}_{suf}", [vp, vp])
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
     if hasattr(lib, "bdx_fused4_tile"):
         _d(lib, "bdx_fused4_tile", [vp, vp])

@@ -43,7 +43,7 @@ class NativeCGRuntime:
         t = op.t
         self._latd = np.ascontiguousarray(pb.latd, dtype=np.int64)
         self._own = np.array(pb.lat.owned_hi, dtype=np.int64)
-        self._ip = np.array([op.version, int(op.affine), pb.degree, t.nq, op.nblocks, op.nty,
+        self._ip = np.array([op.version, op.affine_code, pb.degree, t.nq, op.nblocks, op.nty,
                              op.ntz, op.sy, op.sz, int(use_graph)], dtype=np.int32)
         self._wts = np.ascontiguousarray(t.wts, dtype=np.float64)
         self._qpts = np.ascontiguousarray(t.qpts, dtype=np.float64)

@@ -42,7 +42,7 @@ def _tol(dt):
 
 # (geometry, kernel version, affine fast path allowed)
 VARIANTS = [("otf", 1, True), ("stored", 1, True), ("otf", 2, True), ("otf", 2, False),
-            ("otf", 3, True), ("otf", 3, False), ("otf", 4, True)]
+            ("otf", 3, True), ("otf", 3, False), ("otf", 4, True), ("otf", 5, True)]
 
 
 def _skip_unsupported(pb, version):
@@ -103,11 +103,11 @@ def _cg_job(comm, nc, P, nreps, geometry, version=1, pert=0.1, runtime="native")
 
 @pytest.mark.parametrize("runtime", ["native", "python"])
 @pytest.mark.parametrize("pert", [0.0, 0.1])
-@pytest.mark.parametrize("version", [1, 2, 3, 4])
+@pytest.mark.parametrize("version", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("ranks", [2, 4, 8])
 def test_fused_partition_invariance_threaded(ranks, version, pert, runtime):
-    if version == 4 and pert:
-        pytest.skip("fused4 needs parallelepiped cells")
+    if version in (4, 5) and pert:
+        pytest.skip(f"fused{version} needs parallelepiped cells")
     if version == 1 and runtime == "native":
         pytest.skip("the native runtime drives fused2/3")
     ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert, runtime)[0]
@@ -117,7 +117,7 @@ def test_fused_partition_invariance_threaded(ranks, version, pert, runtime):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
 
 
-@pytest.mark.parametrize("version", [1, 2, 3, 4])
+@pytest.mark.parametrize("version", [1, 2, 3, 4, 5])
 def test_fused_golden_and_mat_comp_16(version):
     if version != 3:  # qmode=0 (phi0 == I) is not a fused3 element
         nx = compute_mesh_size(1000, 3)
@@ -149,7 +149,7 @@ def test_fused3_cg_all_degrees(P, nc, pert):
     assert rel < 1e-10, rel
 
 
-@pytest.mark.parametrize("kernel", ["fused4", "fused3", "fused2", "v1"])
+@pytest.mark.parametrize("kernel", ["fused5", "fused4", "fused3", "fused2", "v1"])
 @pytest.mark.parametrize("nc,P,pert", [((4, 5, 7), 3, 0.0), ((3, 4, 5), 6, 0.1), ((5, 6, 6), 2, 0.0),
                                        ((9, 13, 10), 3, 0.0)])
 def test_random_coefficients_gpu(kernel, nc, P, pert):
@@ -158,6 +158,8 @@ def test_random_coefficients_gpu(kernel, nc, P, pert):
     gpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "gpu", pert, "random")
     if kernel == "fused4" and not (P == 3 and pert == 0.0):
         pytest.skip("fused4: Q3 parallelepiped cells")
+    if kernel == "fused5" and not (P >= 3 and pert == 0.0):
+        pytest.skip("fused5: P >= 3 parallelepiped cells")
     cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", pert, "random")
     rng = np.random.default_rng(5)
     u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
@@ -224,6 +226,84 @@ def _cg_job_shear(comm, nc, nreps):
 def test_fused4_sheared_partition_invariance(ranks):
     ref = run_threaded(1, _cg_job_shear, (8, 8, 16), 12)[0]
     got = run_threaded(ranks, _cg_job_shear, (8, 8, 16), 12)
+    for r in got:
+        for a, b in zip(r, ref):
+            assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
+
+
+F5_CASES = [
+    # ncells, P, qmode, gauss, shear, dtype   (fused5 tiles: P3 4x4, P4 2x4, P>=5 2x2)
+    ((3, 5, 6), 3, 1, False, 0.0, torch.float64),
+    ((4, 9, 7), 3, 0, False, 0.0, torch.float64),
+    ((4, 8, 8), 3, 1, True, 0.375, torch.float64),
+    ((3, 3, 5), 4, 1, False, 0.0, torch.float64),
+    ((2, 4, 8), 4, 0, False, 0.75, torch.float64),
+    ((3, 3, 5), 5, 1, True, 0.0, torch.float64),
+    ((2, 4, 4), 5, 1, False, 0.25, torch.float64),
+    ((3, 3, 5), 6, 1, False, 0.0, torch.float64),
+    ((2, 5, 3), 6, 0, False, 0.0, torch.float64),
+    ((4, 2, 4), 6, 1, False, 0.5, torch.float64),
+    ((2, 3, 3), 7, 1, False, 0.0, torch.float64),
+    ((2, 2, 4), 7, 1, True, 0.125, torch.float64),
+    ((4, 5, 7), 3, 1, False, 0.0, torch.float32),
+    ((3, 5, 3), 6, 1, False, 0.0, torch.float32),
+    ((2, 4, 4), 6, 1, False, 0.25, torch.float32),
+    ((3, 3, 3), 7, 1, False, 0.0, torch.float32),
+]
+
+
+@pytest.mark.parametrize("coef", ["constant", "random"])
+@pytest.mark.parametrize("nc,P,qm,g,shear,dt", F5_CASES)
+def test_fused5_action_and_cg(nc, P, qm, g, shear, dt, coef):
+    """fused5 (nodal Kronecker core): axis-aligned boxes take the 2-array
+    instance, sheared parallelepipeds the 4-array one; action vs the C++ CPU
+    operator and CG vs the host CG."""
+    from benchmark_dolfinx_amd.models.fused import fused_supported
+    gpu = PoissonProblem(Comm(), nc, P, qm, g, dt, "gpu", 0.0, coef, shear)
+    cpu = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "cpu", 0.0, coef, shear)
+    assert gpu.all_affine and fused_supported(gpu, 5)
+    op = FusedLaplacianGPU(gpu, "otf", 5)
+    assert op.affine_code == (2 if shear == 0.0 else 1)
+    rng = np.random.default_rng(17)
+    u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
+    yc = cpu.new_vector()
+    MatFreeLaplacianCPU(cpu).apply(u64, yc)
+    yg = torch.full(gpu.lat.shape, float("nan"), dtype=dt, device=gpu.device)
+    op.apply(u64.to(gpu.device, dt), yg)
+    o = cpu.owned
+    yg = yg.double().cpu()
+    assert torch.isfinite(o(yg)).all()
+    err = (o(yg) - o(yc)).abs().max().item()
+    assert err <= _tol(dt) * 50 * max(1.0, yc.abs().max().item()), err
+    if dt == torch.float64:
+        xg = gpu.new_vector()
+        DeviceCG(gpu).solve(op, xg, gpu.assemble_rhs(), 15)
+        xc = cpu.new_vector()
+        cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 15)
+        rel = (o(xg.cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
+        assert rel < 1e-10, rel
+    op.close()
+
+
+def _cg_job_f5(comm, nc, P, nreps, shear):
+    pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", 0.0, "random", shear)
+    u = pb.assemble_rhs()
+    x = pb.new_vector()
+    op = FusedLaplacianGPU(pb, "otf", 5)
+    DeviceCG(pb).solve(op, x, u, nreps)
+    y = pb.new_vector()
+    op.apply(u, y)
+    torch.cuda.synchronize()
+    op.close()
+    return pb.norm(u), pb.norm(x), pb.norm(y)
+
+
+@pytest.mark.parametrize("P,nc", [(6, (4, 4, 8)), (4, (8, 4, 8))])
+@pytest.mark.parametrize("shear", [0.0, 0.5])
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_fused5_partition_invariance(ranks, shear, P, nc):
+    ref = run_threaded(1, _cg_job_f5, nc, P, 10, shear)[0]
+    got = run_threaded(ranks, _cg_job_f5, nc, P, 10, shear)
     for r in got:
         for a, b in zip(r, ref):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
