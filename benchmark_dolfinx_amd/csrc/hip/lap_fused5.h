@@ -55,23 +55,27 @@ constexpr int kF5Stride = 8;
 constexpr int kF5Tab = 4 * 64;
 static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
 
-template <int ND> struct F5Tile;  // cells per wave and (y, z) tile per degree
-template <> struct F5Tile<4> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
-template <> struct F5Tile<5> { static constexpr int CPW = 2, TY = 2, TZ = 4; };
-template <> struct F5Tile<6> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+// cells per wave and (y, z) tile per degree; NARR = 4 (sheared cells) keeps
+// the 2 x 2 tile at ND >= 6 (its per-wave buffers are twice as large)
+template <int ND, int NARR> struct F5Tile;
+template <int NARR> struct F5Tile<4, NARR> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
+template <int NARR> struct F5Tile<5, NARR> { static constexpr int CPW = 2, TY = 2, TZ = 4; };
+template <int NARR> struct F5Tile<6, NARR> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 #ifndef BDX_F5_TY7
 #define BDX_F5_TY7 2
 #endif
 #ifndef BDX_F5_TZ7
 #define BDX_F5_TZ7 2
 #endif
-template <> struct F5Tile<7> { static constexpr int CPW = 1, TY = BDX_F5_TY7, TZ = BDX_F5_TZ7; };
-template <> struct F5Tile<8> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+template <> struct F5Tile<7, 2> { static constexpr int CPW = 1, TY = BDX_F5_TY7, TZ = BDX_F5_TZ7; };
+template <> struct F5Tile<7, 4> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+template <int NARR> struct F5Tile<8, NARR> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 
 template <typename T, int ND, int NARR>
 struct F5Shape {
   static constexpr int P = ND - 1;
-  static constexpr int CPW = F5Tile<ND>::CPW, TY = F5Tile<ND>::TY, TZ = F5Tile<ND>::TZ;
+  static constexpr int CPW = F5Tile<ND, NARR>::CPW, TY = F5Tile<ND, NARR>::TY,
+                       TZ = F5Tile<ND, NARR>::TZ;
   static constexpr int CELLS = TY * TZ;
   static_assert(CELLS % CPW == 0, "whole waves of cells");
   static constexpr int WAVES = CELLS / CPW;
@@ -190,7 +194,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
   };
 
   // ---- per-thread staging descriptors (planes 1..P of a layer)
-  int st_goff[NPF], st_meta[NPF];
+  // 32-bit unsigned per-layer offsets: uniform base + zero-extended VGPR
+  // offset (SADDR addressing, no 64-bit address VGPRs per element)
+  unsigned st_goff[NPF];
+  int st_meta[NPF];
 #pragma unroll
   for (int k = 0; k < NPF; ++k) {
     const int e = tid + k * NT;
@@ -199,7 +206,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     if (e < P * PL) {
       const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
       const int f = yz_flags(ly, lz);
-      st_goff[k] = (pl * Ly + y0 + ly) * ld + z0 + lz;
+      st_goff[k] = static_cast<unsigned>((pl * Ly + y0 + ly) * ld + z0 + lz);
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
   }
@@ -327,6 +334,9 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
 
     // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
     const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
+    const T* __restrict__ un_r = A.u + lnext;
+    const T* __restrict__ un_p = A.pold + lnext;
+    T* __restrict__ un_x = A.x + lnext;
     T pf_r[NPF], pf_p[NPF], pf_x[NPF];
     T pf_v[NPV];
 #pragma unroll
@@ -335,10 +345,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
       pf_p[k] = T(0);
       pf_x[k] = T(0);
       if (!(BDX_F5_DROP & 4) && !last && (st_meta[k] & kValid)) {
-        pf_r[k] = A.u[lnext + st_goff[k]];
+        pf_r[k] = un_r[st_goff[k]];
         if constexpr (MODE == kFusedCG) {
-          pf_p[k] = A.pold[lnext + st_goff[k]];
-          if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = A.x[lnext + st_goff[k]];
+          pf_p[k] = un_p[st_goff[k]];
+          if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = un_x[st_goff[k]];
         }
       }
     }
@@ -548,7 +558,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
             if constexpr (MODE == kFusedCG) {
               if (m & kOwnT) {
                 pnl[st_goff[k]] = val;
-                if (xupd) A.x[lnext + st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
+                if (xupd) un_x[st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
               }
             }
             if ((m & kBcYZ) || gxx == A.bcx_hi) {
@@ -701,8 +711,8 @@ inline const T* f5_tables_on_device(T* sym_addr_holder, const void* sym, const T
                                                   T* out) {                        \
     return pack_tables5<T>(nd, nq, phi0, Dd, wts, out);                            \
   }                                                                                \
-  extern "C" int bdx_fused5_tile_p##PP##_##SUF(int* ty, int* tz) {                 \
-    *ty = F5Tile<PP + 1>::TY;                                                      \
-    *tz = F5Tile<PP + 1>::TZ;                                                      \
+  extern "C" int bdx_fused5_tile_p##PP##_##SUF(int affine_ok, int* ty, int* tz) {  \
+    *ty = affine_ok == 2 ? F5Tile<PP + 1, 2>::TY : F5Tile<PP + 1, 4>::TY;          \
+    *tz = affine_ok == 2 ? F5Tile<PP + 1, 2>::TZ : F5Tile<PP + 1, 4>::TZ;          \
     return 0;                                                                      \
   }

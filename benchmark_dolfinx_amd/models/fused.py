@@ -84,7 +84,7 @@ class FusedLaplacianGPU:
             _check(self.lib.bdx_fused4_tile(ctypes.byref(ty), ctypes.byref(tz)), "fused4_tile")
         elif version == 5:
             _check(getattr(self.lib, f"bdx_fused5_tile_p{pb.degree}_{pb.suf}")(
-                ctypes.byref(ty), ctypes.byref(tz)), "fused5_tile")
+                self.affine_code, ctypes.byref(ty), ctypes.byref(tz)), "fused5_tile")
         else:
             _check(self.lib.bdx_fused_tile(t.nq, ctypes.byref(ty), ctypes.byref(tz)),
                    "fused_tile")

@@ -53,7 +53,7 @@ def declare(lib) -> None:
         for P in range(1, 8):
             if hasattr(lib, f"bdx_fused5_tables_{suf}_p{P}"):
                 _d(lib, f"bdx_fused5_tables_{suf}_p{P}", [i32, i32, vp, vp, vp, vp])
-                _d(lib, f"bdx_fused5_tile_p{P}_{suf}", [vp, vp])
+                _d(lib, f"bdx_fused5_tile_p{P}_{suf}", [i32, vp, vp])
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
     if hasattr(lib, "bdx_fused4_tile"):
         _d(lib, "bdx_fused4_tile", [vp, vp])

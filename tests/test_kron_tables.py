@@ -48,8 +48,10 @@ def test_fused5_tables(P, qmode, gauss, suf, npdt):
         np.testing.assert_allclose(blk[b, :nd, :nd], ref, atol=tol * np.abs(ref).max())
         assert not blk[b, nd:, :].any() and not blk[b, :, nd:].any()
     ty, tz = ctypes.c_int(0), ctypes.c_int(0)
-    assert getattr(lib, f"bdx_fused5_tile_p{P}_{suf}")(ctypes.byref(ty), ctypes.byref(tz)) == 0
-    assert ty.value >= 1 and tz.value >= 1
+    for code in (1, 2):
+        assert getattr(lib, f"bdx_fused5_tile_p{P}_{suf}")(code, ctypes.byref(ty),
+                                                           ctypes.byref(tz)) == 0
+        assert ty.value >= 1 and tz.value >= 1
 
 
 @pytest.mark.parametrize("P", [2, 3, 5])
