@@ -297,9 +297,9 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
 
   // wave-local LDS exchange between passes (a wave's lanes run in lockstep)
   auto wave_sync = [&]() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   };
   // 1D matrices (kernarg: wave-uniform scalar loads): id 0 = M, 1 = K, 2 = C
   // The tables (a device copy, see f5_tables_on_device) are read through a
@@ -327,6 +327,9 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     }
   };
 
+  const int64_t kc_ps = static_cast<int64_t>(A.n1) * A.n2;
+  const int64_t kc_cell = static_cast<int64_t>(ty * TY + cy) * A.n2 + tz * TZ + cz;
+  T kc_cur = (A.kc && cell_on) ? A.kc[kc_cell] : A.kappa;
   for (int cx = 0; cx < ncx; ++cx) {
     const int cur = cx & 1, nxt = cur ^ 1;
     const bool last = (cx == ncx - 1);
@@ -339,6 +342,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     T* __restrict__ un_x = A.x + lnext;
     T pf_r[NPF], pf_p[NPF], pf_x[NPF];
     T pf_v[NPV];
+    // next layer's cell coefficient rides with the prefetch: a load consumed
+    // in the same layer would make the wave wait for the whole batch
+    T kc_nxt = kc_cur;
+    if (A.kc && !last && cell_on) kc_nxt = A.kc[static_cast<int64_t>(cx + 1) * kc_ps + kc_cell];
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
       pf_r[k] = T(0);
@@ -383,11 +390,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
       const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
       const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
       const T det = J00 * K00 + J01 * K10 + J02 * K20;
-      const T kcell = A.kc ? (cell_on ? A.kc[(static_cast<int64_t>(cx) * A.n1 + ty * TY + cy) * A.n2 +
-                                            tz * TZ + cz]
-                                      : T(0))
-                           : A.kappa;
-      const T sc = cell_on ? kcell * fast_rcp(det) : T(0);
+      const T sc = cell_on ? kc_cur * fast_rcp(det) : T(0);
       G00 = sc * (K00 * K00 + K01 * K01 + K02 * K02);
       G01 = sc * (K00 * K10 + K01 * K11 + K02 * K12);
       G02 = sc * (K00 * K20 + K01 * K21 + K02 * K22);
@@ -587,6 +590,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
         if (e < NV) s_X[nxt][NV + e] = pf_v[k];
       }
     }
+    kc_cur = kc_nxt;
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
