@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   __shared__ T s_c[2][PL];
   __shared__ T s_e[EB + 1];
   __shared__ T s_X[2][2 * NV];
+  __shared__ T s_kc[2][CELLS];  // per-cell coefficient, double buffered
   __shared__ double s_red[16];
 
   const int tid = threadIdx.x;
@@ -194,7 +195,9 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     if (e < P * PL) {
       const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
       const int f = yz_flags(ly, lz);
-      st_goff[k] = (pl * Ly + y0 + ly) * ld + z0 + lz;
+      // invalid (off-lattice) slots keep offset 0: the prefetch loads them
+      // unconditionally (in bounds, value unused)
+      if (f & kValid) st_goff[k] = (pl * Ly + y0 + ly) * ld + z0 + lz;
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
   }
@@ -286,7 +289,12 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
 
   const int64_t kc_ps = static_cast<int64_t>(A.n1) * A.n2;
   const int64_t kc_cell = static_cast<int64_t>(ty * TY + cy) * A.n2 + tz * TZ + cz;
-  T kc_cur = (A.kc && cell_on) ? A.kc[kc_cell] : A.kappa;
+  if (A.kc) s_kc[0][c] = cell_on ? A.kc[kc_cell] : T(0);  // read after the loop-top barrier
+  // Everything loaded so far (the per-lane x matrices Xr, the prologue
+  // layer) has landed before the march starts: without this explicit wait the
+  // waitcnt pass carries the Xr loads as pending around the loop and makes
+  // their uses inside the MFMA core wait for each layer's prefetch batch.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   for (int cx = 0; cx < ncx; ++cx) {
     const int cur = cx & 1, nxt = cur ^ 1;
     const bool last = (cx == ncx - 1);
@@ -298,18 +306,22 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     T pf_v[NPV];
     // next layer's cell coefficient rides with the prefetch (a load consumed
     // in the same layer would make the wave wait for the whole batch)
-    T kc_nxt = kc_cur;
+    T kc_nxt = T(0);
     if (A.kc && !last && cell_on) kc_nxt = A.kc[static_cast<int64_t>(cx + 1) * kc_ps + kc_cell];
+    // Unconditional loads (the last layer re-reads layer 0, unused): a
+    // per-slot conditional load makes the register allocator copy
+    // half-loaded pairs, and each copy waits for its load.
+    const int64_t lpf = last ? 0 : lnext;
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
-      if (!(BDX_F4_DROP & 4) && !last && (st_meta[k] & kValid)) {
-        pf_r[k] = A.u[lnext + st_goff[k]];
+      if constexpr ((BDX_F4_DROP & 4) == 0) {
+        pf_r[k] = A.u[lpf + st_goff[k]];
         if constexpr (MODE == kFusedCG) {
-          pf_p[k] = A.pold[lnext + st_goff[k]];
-          if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = A.x[lnext + st_goff[k]];
+          pf_p[k] = A.pold[lpf + st_goff[k]];
+          if (xupd) pf_x[k] = A.x[lpf + st_goff[k]];
         }
       }
     }
@@ -351,7 +363,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
       const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
       const T det = J00 * K00 + J01 * K10 + J02 * K20;
-      const T sc = cell_on ? kc_cur * fast_rcp(det) : T(0);
+      const T kcell = A.kc ? s_kc[cur][c] : A.kappa;
+      const T sc = cell_on ? kcell * fast_rcp(det) : T(0);
       G00 = sc * (K00 * K00 + K01 * K01 + K02 * K02);
       G01 = sc * (K00 * K10 + K01 * K11 + K02 * K12);
       G02 = sc * (K00 * K20 + K01 * K21 + K02 * K22);
@@ -439,6 +452,55 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     }
     __syncthreads();
 
+    // ------------------------------------------------ stage the next layer (LDS)
+    // The prefetched values go to LDS before any global store of this layer
+    // is issued: vmcnt retires in order, so the wait for the prefetch batch
+    // never includes a store, and the stores below (gather, then the staging
+    // writes) drain while the next layer computes.  The wait is explicit and
+    // unconditional (vmcnt(0) only; gfx9 encoding) so the waitcnt pass sees
+    // no prefetch register pending on any path after this point.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    if (!last) {
+      T* __restrict__ un = s_u[nxt];
+#pragma unroll
+      for (int k = 0; k < NCP; ++k)
+        if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
+      // branch-free: every prefetch register is rewritten here by a VALU op,
+      // so no later store can find one of them still pending (the waitcnt
+      // pass is conservative across branches)
+#pragma unroll
+      for (int k = 0; k < NPF; ++k) {
+        const int m = st_meta[k];
+        const int gxx = (cx + 1) * P + ((m >> 4) & 15);
+        T val;
+        if constexpr (MODE == kFusedCG) {
+          val = pf_r[k] + beta * pf_p[k];
+          pf_x[k] += xalpha * pf_p[k];
+        } else {
+          val = pf_r[k];
+        }
+        pf_r[k] = val;  // p (CG) / u (action) of the node: stored below
+        const bool bcn = (m & kBcYZ) || gxx == A.bcx_hi;
+        if constexpr (MODE == kFusedCG) {
+          const bool rown = (m & kValid) && (m & kOwnT) && (m & kRownYZ) && gxx < A.ownx;
+          pap += (bcn && rown) ? static_cast<double>(val) * static_cast<double>(val) : 0.0;
+        }
+        const T v = ((m & kValid) && !bcn) ? val : T(0);
+        if (tid + k * NT < P * PL) un[m >> 8] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < NPV; ++k) {
+        const int e = tid + k * NT;
+        if (e < NV) s_X[nxt][e] = sX[NV + e];
+      }
+#pragma unroll
+      for (int k = 0; k < NPV; ++k) {
+        const int e = tid + k * NT;
+        if (e < NV) s_X[nxt][NV + e] = pf_v[k];
+      }
+      if (A.kc) s_kc[nxt][c] = kc_nxt;  // (the prefetch batch has landed here)
+    }
+
     // ------------------------------------------------ gather-sum and write out
     if constexpr ((BDX_F4_DROP & 2) == 0) {
       const int64_t lbase = static_cast<int64_t>(cx) * P;
@@ -468,60 +530,26 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       }
     }
 
-    // ------------------------------------------------ stage the next layer
+    // ------------------------------------------------ staging stores
     if (!last) {
-      T* __restrict__ un = s_u[nxt];
-#pragma unroll
-      for (int k = 0; k < NCP; ++k)
-        if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
       T* __restrict__ pnl = A.pnew + lnext;
       T* __restrict__ yl = A.y + lnext;
 #pragma unroll
       for (int k = 0; k < NPF; ++k) {
         const int m = st_meta[k];
-        if (tid + k * NT < P * PL) {
-          T v = T(0);
-          if (m & kValid) {
-            const int gxx = (cx + 1) * P + ((m >> 4) & 15);
-            T val;
-            if constexpr (MODE == kFusedCG) {
-              val = pf_r[k] + beta * pf_p[k];
-            } else {
-              val = pf_r[k];
-            }
-            if constexpr (MODE == kFusedCG) {
-              if (m & kOwnT) {
-                pnl[st_goff[k]] = val;
-                if (xupd) A.x[lnext + st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
-              }
-            }
-            if ((m & kBcYZ) || gxx == A.bcx_hi) {
-              if (m & kOwnT) {
-                const bool rown = (m & kRownYZ) && gxx < A.ownx;
-                yl[st_goff[k]] = rown ? val : T(0);
-                if constexpr (MODE == kFusedCG) {
-                  if (rown) pap += static_cast<double>(val) * static_cast<double>(val);
-                }
-              }
-              val = T(0);
-            }
-            v = val;
+        if (tid + k * NT < P * PL && (m & kValid) && (m & kOwnT)) {
+          const int gxx = (cx + 1) * P + ((m >> 4) & 15);
+          if constexpr (MODE == kFusedCG) {
+            pnl[st_goff[k]] = pf_r[k];
+            if (xupd) A.x[lnext + st_goff[k]] = pf_x[k];
           }
-          un[m >> 8] = v;
+          if ((m & kBcYZ) || gxx == A.bcx_hi) {
+            const bool rown = (m & kRownYZ) && gxx < A.ownx;
+            yl[st_goff[k]] = rown ? pf_r[k] : T(0);
+          }
         }
       }
-#pragma unroll
-      for (int k = 0; k < NPV; ++k) {
-        const int e = tid + k * NT;
-        if (e < NV) s_X[nxt][e] = sX[NV + e];
-      }
-#pragma unroll
-      for (int k = 0; k < NPV; ++k) {
-        const int e = tid + k * NT;
-        if (e < NV) s_X[nxt][NV + e] = pf_v[k];
-      }
     }
-    kc_cur = kc_nxt;
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
