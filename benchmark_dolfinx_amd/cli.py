@@ -9,8 +9,9 @@ Reference options (src/main.cpp:144-183): --platform, --float, --ndofs,
 --geom_perturb_fact, --use_gauss, --json.  Unknown options are accepted
 (like `allow_unregistered`, used for `SPDLOG_LEVEL=...`).
 
-MI355X extensions (additive): --kernel {auto,fused,v1}, --geometry
-{auto,otf,stored}, --warmup N (untimed repetitions before the timed loop).
+MI355X extensions (additive): --kernel {auto,fused5,fused4,fused3,fused2,
+fused,v1}, --geometry {auto,otf,otf-general,stored}, --kappa {constant,random},
+--warmup N (untimed repetitions before the timed loop).
 The JSON gains an additive "mi355x" object; the reference keys are
 unchanged.
 """

@@ -498,6 +498,44 @@ int bdx_rt_nccl_unique_id(void* out128) {
   return static_cast<int>(sizeof(id));
 }
 
+// Hardware self-test of the RCCL transport on one GPU (a 1-rank communicator):
+// the grouped send/recv of RcclTransport::exchange to itself (buf[0, n) ->
+// buf[n, 2n)), the device-scalar all-reduce of buf[2n, 2n+2), then the same
+// pair captured into a hipGraph and replayed (into buf[2n+2, 3n+2)).  The
+// multi-rank loop issues the identical calls over xGMI.  Returns 0 on success.
+int bdx_rt_rccl_selftest(double* buf, int n, hipStream_t st) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -10;
+  RcclTransport t;
+  t.nranks = 1;
+  if (ncclCommInitRank(&t.comm, 1, id, 0) != ncclSuccess) return -11;
+  const std::vector<int64_t> cnt{n}, off0{0}, offn{n}, offg{2 * static_cast<int64_t>(n) + 2};
+  int rc = t.exchange(buf, cnt, off0, buf, cnt, offn, sizeof(double), st);
+  if (!rc) rc = t.allreduce_sum(buf + 2 * n, 2, st);
+  if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = -12;
+  if (rc) return rc;
+  // capture on an own non-blocking stream, as the runtime does (the caller's
+  // stream may be the legacy default stream, which cannot be captured)
+  hipStream_t cs = nullptr;
+  if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return -13;
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    hipStreamDestroy(cs);
+    return -14;
+  }
+  rc = t.exchange(buf, cnt, off0, buf, cnt, offg, sizeof(double), cs);
+  if (!rc) rc = t.allreduce_sum(buf + 2 * n, 2, cs);
+  if (hipStreamEndCapture(cs, &g) != hipSuccess || !g) rc = rc ? rc : -15;
+  if (!rc && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) rc = -16;
+  if (!rc && hipGraphLaunch(ge, cs) != hipSuccess) rc = -17;
+  if (!rc && hipStreamSynchronize(cs) != hipSuccess) rc = -18;
+  if (ge) hipGraphExecDestroy(ge);
+  if (g) hipGraphDestroy(g);
+  hipStreamDestroy(cs);
+  return rc;
+}
+
 void* bdx_rt_create(int is_f64, const int64_t* latd, const int64_t* own, const int* iparams,
                     double kappa, const double* wts, const double* qpts, const void* tabs,
                     void* const* ptrs, const int64_t* halo_sizes, const int64_t* face_cnt,

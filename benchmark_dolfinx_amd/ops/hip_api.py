@@ -59,6 +59,7 @@ def declare(lib) -> None:
         _d(lib, "bdx_fused4_tile", [vp, vp])
     # native CG runtime (runtime.hip)
     _d(lib, "bdx_rt_nccl_unique_id", [vp])
+    _d(lib, "bdx_rt_rccl_selftest", [vp, i32, vp])
     _d(lib, "bdx_rt_create", [i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
                               vp, i64, vp], vp)
     _d(lib, "bdx_rt_reset", [vp])
