@@ -38,6 +38,15 @@
 // Timing-only phase drops for A/B attribution (wrong numerics when nonzero):
 // 1 = MFMA core, 2 = gather + write-out, 4 = next-layer global loads,
 // 8 = x contraction + geometry.
+#ifndef BDX_F4_RP
+#define BDX_F4_RP 4
+#endif
+#ifndef BDX_F4_P1
+#define BDX_F4_P1 17
+#endif
+#ifndef BDX_F4_PC
+#define BDX_F4_PC 72
+#endif
 #ifndef BDX_F4_NOSKIP
 #define BDX_F4_NOSKIP 0
 #endif
@@ -80,9 +89,12 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   constexpr int NCP = (PL + NT - 1) / NT;
   constexpr int NV = (TY + 1) * (TZ + 1) * 3;
   constexpr int NPV = (NV + NT - 1) / NT;
-  // element-vector scratch [cell][j][k][i]: odd pitches spread the gather's
-  // lz-consecutive reads over the LDS banks
-  constexpr int RP = 5, P1 = 21, PC = 85;
+  // element-vector scratch [cell][j][k][i]; pitches from an exhaustive search
+  // of the gather reads + element-vector writes with the gfx950 bank model
+  // (b64: 2 x 32 lanes, 64 banks; scripts/lds_bank_f4.py): 135 LDS cycles per
+  // workgroup layer vs 257 for the earlier odd pitches (5, 21, 85), ideal 112; the
+  // same-box A/B is neutral (38.50 vs 38.47 GDoF/s): LDS is not the limiter
+  constexpr int RP = BDX_F4_RP, P1 = BDX_F4_P1, PC = BDX_F4_PC;
   constexpr int EB = CELLS * PC;
   constexpr int ZSLOT = EB;
   static_assert(ZSLOT < 32768, "16-bit LDS source offsets");
