@@ -23,6 +23,12 @@ int pack_tables(const double* phi0, const double* dphi1, T* out) {
 }
 
 
+// Timing-only drops for A/B attribution (wrong numerics when nonzero):
+// 1 = tile-interface fold, 2 = r.r (scripts/job_upddrop.sh)
+#ifndef BDX_UPD_DROP
+#define BDX_UPD_DROP 0
+#endif
+
 // CG update of the fused2 path: alpha = s[rn] / s[pap];
 //   r -= alpha (y + interface partials);  partial r.r
 // The tile-interface partials (YB/ZB/CB) are folded here on the fly instead of
@@ -68,6 +74,7 @@ __global__ void __launch_bounds__(256)
         const int k = k0 + e;
         if (k >= o2) break;
         T v = full ? vy[e] : y[base + k];
+#if (BDX_UPD_DROP & 1) == 0
         if (yrow >= 0) v += ybr[k];
         int zq = static_cast<int>(static_cast<float>(k) * inv_sz);
         if (zq * sz > k) --zq;
@@ -76,12 +83,15 @@ __global__ void __launch_bounds__(256)
           v += zbr[zq - 1];
           if (yrow >= 0) v += cbr[zq - 1];
         }
+#endif
         const T rn = (full ? vr[e] : r[base + k]) - alpha * v;
         if (full)
           vr[e] = rn;
         else
           r[base + k] = rn;
+#if (BDX_UPD_DROP & 2) == 0
         acc += static_cast<double>(rn) * static_cast<double>(rn);
+#endif
       }
       if (full) *reinterpret_cast<V*>(r + base + k0) = vr;
     }
