@@ -157,7 +157,7 @@ int grid_for_rows(int64_t nrows) {
 
 extern "C" {
 
-int bdx_hip_partials_size() { return 2048; }
+int bdx_hip_partials_size() { return 65536; }  // >= kPartialsCap (fused_common.hip)
 
 // Fixed-order reduction of n per-block partials into out[slot].
 int bdx_reduce_partials(const double* partials, int n, double* out, int slot,

@@ -29,6 +29,21 @@ int pack_tables(const double* phi0, const double* dphi1, T* out) {
 #define BDX_UPD_DROP 0
 #endif
 
+// Flat non-persistent update pass (1) or the row kernel (0); kPartialsCap is
+// the partials capacity every caller provides (bdx_hip_partials_size).  The
+// flat pass wants a non-persistent grid (a persistent 8192/16384-block
+// grid-stride version measured 1.70 ms vs 1.52 at Q3); its up to 65280 block
+// partials are summed in two fixed-order stages (256 slices into the last 256
+// slots of the partials buffer, then one block): deterministic like the rest.
+#ifndef BDX_UPD_FLAT
+#define BDX_UPD_FLAT 1
+#endif
+constexpr int kPartialsCap = 65536, kStage1 = 256;
+#ifndef BDX_UPD_GRID
+#define BDX_UPD_GRID (kPartialsCap - kStage1)
+#endif
+static_assert(BDX_UPD_GRID <= kPartialsCap - kStage1, "update grid exceeds the partials capacity");
+
 // CG update of the fused2 path: alpha = s[rn] / s[pap];
 //   r -= alpha (y + interface partials);  partial r.r
 // The tile-interface partials (YB/ZB/CB) are folded here on the fly instead of
@@ -100,6 +115,78 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
+// Flat variant of the update (BDX_UPD_FLAT): the owned rows j < o1 of an
+// x-plane are one contiguous block of o1 * ld elements (row pitch ld, a
+// multiple of 16 elements: no 16-byte vector straddles two rows), so the pass
+// runs as a plain stream -- one chunk of 256 threads x 2 vectors per block,
+// blocks up to the partials capacity (grid-stride beyond), both loads of a
+// thread in flight before any arithmetic.  Same arithmetic per element as the
+// row kernel above (fold, r update, r.r); columns k >= o2 are left as read.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cg_update_flat_kernel(int64_t L1, int64_t ld, int64_t o0, int64_t o1, int64_t o2,
+                          int64_t Lz, T* __restrict__ r, const T* __restrict__ y,
+                          const T* __restrict__ yb, const T* __restrict__ zb,
+                          const T* __restrict__ cb, int nty, int ntz, int sy, int sz,
+                          const double* __restrict__ scal, int rn_slot, int pap_slot,
+                          double* __restrict__ partials) {
+  __shared__ double lds[16];
+  const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
+  constexpr int W = 16 / sizeof(T), U = 2, CH = 256 * U;
+  typedef T V __attribute__((ext_vector_type(W)));
+  const int ldv = static_cast<int>(ld / W);
+  const int nvp = static_cast<int>(o1) * ldv;
+  const int nch = (nvp + CH - 1) / CH;
+  const int64_t nwork = o0 * nch;
+  const float inv_sz = 1.0f / static_cast<float>(sz);
+  const float inv_ldv = 1.0f / static_cast<float>(ldv);
+  double acc = 0.0;
+  for (int64_t c = blockIdx.x; c < nwork; c += gridDim.x) {
+    const int64_t i = c / nch;
+    const int v0 = static_cast<int>(c - i * nch) * CH + static_cast<int>(threadIdx.x) * U;
+    const int64_t pbase = i * L1 * ld;
+    V vy[U], vr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v0 + u < nvp) {
+        vy[u] = *reinterpret_cast<const V*>(y + pbase + static_cast<int64_t>(v0 + u) * W);
+        vr[u] = *reinterpret_cast<const V*>(r + pbase + static_cast<int64_t>(v0 + u) * W);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = v0 + u;
+      if (v >= nvp) continue;
+      int j = static_cast<int>(static_cast<float>(v) * inv_ldv);
+      if (j * ldv > v) --j;
+      if ((j + 1) * ldv <= v) ++j;
+      const int k0 = (v - j * ldv) * W;
+      const int tyy = j / sy;
+      const int yrow = (j - tyy * sy == 0 && tyy >= 1 && tyy < nty) ? tyy - 1 : -1;
+#pragma unroll
+      for (int e = 0; e < W; ++e) {
+        const int k = k0 + e;
+        if (k >= o2) continue;
+        T t = vy[u][e];
+        if (yrow >= 0) t += yb[(i * (nty - 1) + yrow) * Lz + k];
+        int zq = static_cast<int>(static_cast<float>(k) * inv_sz);
+        if (zq * sz > k) --zq;
+        if ((zq + 1) * sz <= k) ++zq;
+        if (zq * sz == k && zq >= 1 && zq < ntz) {
+          t += zb[(i * L1 + j) * (ntz - 1) + zq - 1];
+          if (yrow >= 0) t += cb[(i * (nty - 1) + yrow) * (ntz - 1) + zq - 1];
+        }
+        const T rn = vr[u][e] - alpha * t;
+        vr[u][e] = rn;
+        acc += static_cast<double>(rn) * static_cast<double>(rn);
+      }
+      *reinterpret_cast<V*>(r + pbase + static_cast<int64_t>(v) * W) = vr[u];
+    }
+  }
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
 // x += (s[num] / s[den]) p over the owned rows (flush of the lagged x update).
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -114,6 +201,18 @@ __global__ void __launch_bounds__(256)
     const int64_t base = (i * L1 + j) * ld;
     for (int64_t k = lane; k < o2; k += 64) x[base + k] += alpha * p[base + k];
   }
+}
+
+// stage 1 of the two-stage sum: block b sums slice b of partials[0, n) into out[b]
+__global__ void reduce_partials_slices(const double* __restrict__ partials, int n,
+                                       double* __restrict__ out) {
+  __shared__ double lds[16];
+  const int per = (n + static_cast<int>(gridDim.x) - 1) / static_cast<int>(gridDim.x);
+  const int lo = static_cast<int>(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
+  double acc = 0.0;
+  for (int i = lo + static_cast<int>(threadIdx.x); i < hi; i += blockDim.x) acc += partials[i];
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) out[blockIdx.x] = t;
 }
 
 __global__ void reduce_partials_fixed(const double* __restrict__ partials, int n,
@@ -139,12 +238,29 @@ extern "C" {
                                 int rn_slot, int pap_slot, int out_slot,            \
                                 double* partials, hipStream_t st) {                 \
     const BdxLattice lat = BdxLattice::from(latd);                                  \
-    const int g = rows_grid(own[0] * own[1]);                                       \
-    cg_update_iface_kernel<T><<<g, 256, 0, st>>>(lat.L[1], lat.ld, own[0], own[1],  \
-                                                 own[2], lat.L[2], r, y, yb, zb, cb, \
-                                                 nty, ntz, sy, sz, scal, rn_slot,   \
-                                                 pap_slot, partials);               \
-    reduce_partials_fixed<<<1, 256, 0, st>>>(partials, g, scal, out_slot);          \
+    int g;                                                                          \
+    if (BDX_UPD_FLAT) {                                                             \
+      const int64_t nvp = own[1] * (lat.ld * static_cast<int64_t>(sizeof(T)) / 16); \
+      const int64_t want = own[0] * ((nvp + 511) / 512);                            \
+      g = static_cast<int>(want < BDX_UPD_GRID ? (want > 0 ? want : 1) : BDX_UPD_GRID); \
+      cg_update_flat_kernel<T><<<g, 256, 0, st>>>(lat.L[1], lat.ld, own[0], own[1], \
+                                                  own[2], lat.L[2], r, y, yb, zb, cb, \
+                                                  nty, ntz, sy, sz, scal, rn_slot,  \
+                                                  pap_slot, partials);              \
+    } else {                                                                        \
+      g = rows_grid(own[0] * own[1]);                                               \
+      cg_update_iface_kernel<T><<<g, 256, 0, st>>>(lat.L[1], lat.ld, own[0], own[1], \
+                                                   own[2], lat.L[2], r, y, yb, zb, cb, \
+                                                   nty, ntz, sy, sz, scal, rn_slot, \
+                                                   pap_slot, partials);             \
+    }                                                                               \
+    if (g > 4 * kStage1) {                                                          \
+      double* stage = partials + kPartialsCap - kStage1;                            \
+      reduce_partials_slices<<<kStage1, 256, 0, st>>>(partials, g, stage);          \
+      reduce_partials_fixed<<<1, 256, 0, st>>>(stage, kStage1, scal, out_slot);     \
+    } else {                                                                        \
+      reduce_partials_fixed<<<1, 256, 0, st>>>(partials, g, scal, out_slot);        \
+    }                                                                               \
     return static_cast<int>(hipGetLastError());                                     \
   }                                                                                 \
   int bdx_xflush_##SUF(const int64_t* latd, const int64_t* own, T* x, const T* p,   \

@@ -47,7 +47,8 @@ class NativeCGRuntime:
                              op.ntz, op.sy, op.sz, int(use_graph)], dtype=np.int32)
         self._wts = np.ascontiguousarray(t.wts, dtype=np.float64)
         self._qpts = np.ascontiguousarray(t.qpts, dtype=np.float64)
-        self.upart = torch.zeros(2048, dtype=torch.float64, device=pb.device)
+        self.upart = torch.zeros(self.lib.bdx_hip_partials_size(), dtype=torch.float64,
+                                 device=pb.device)
         fo, gh = halo.owned_faces, halo.ghosts
         bufs = [cg.x, cg.r, op.p_old, op.p_new, cg.y, op.yb, op.zb, op.cb, pb.xv, cg.scal,
                 op.partials, self.upart, halo.buf_a, halo.buf_b, fo.table, gh.table, pb.kc]
