@@ -144,6 +144,18 @@ def main(argv=None) -> int:
     return 0
 
 
+def _device_name() -> str:
+    import torch
+
+    from .ops.kernels import device_name
+    return device_name(torch.cuda.current_device())
+
+
+def _build_flags() -> dict:
+    from .ops.native import build_flags
+    return build_flags()
+
+
 def run_benchmark(comm, nx, args, platform):
     import torch
 
@@ -162,7 +174,8 @@ def run_benchmark(comm, nx, args, platform):
            "z_norm": res.znorm, "gdof_per_second": gdofs}
     extra = {"gdof_per_second_per_gpu": gdofs / comm.size, "mesh": list(nx),
              "partition": list(pb.lat.pgrid), "e_norm": res.enorm,
-             "device": torch.cuda.get_device_name() if platform == "gpu" else "cpu",
+             "device": _device_name() if platform == "gpu" else "cpu",
+             "build_flags": _build_flags() if platform == "gpu" else None,
              **res.extra}
     return out, extra
 

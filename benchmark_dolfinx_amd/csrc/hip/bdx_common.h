@@ -14,6 +14,10 @@
 
 constexpr int kMaxNd = 8;
 constexpr int kMaxNq = 9;
+// packed 1D-table capacity of every fused kernel family (the largest: fused
+// v1 TAB for nd=8, nq=9 at the f32 pitch); the runtime copies this many
+// entries
+constexpr int kFusedTabMax = 2 * 9 * 12 + 9 * 8 + 8 * 12;
 
 enum { kGeomStored = 0, kGeomOTF = 1 };
 

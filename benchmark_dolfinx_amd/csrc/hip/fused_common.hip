@@ -274,6 +274,9 @@ BDX_CGI(double, f64)
 BDX_CGI(float, f32)
 #undef BDX_CGI
 
+// Timing-only phase drops compiled into this TU (0 in a valid build).
+int bdx_drop_flags_common() { return BDX_UPD_DROP; }
+
 // Tile shape (cells in y, z) used by the fused kernel for a given nq.
 int bdx_fused_tile(int nq, int* ty, int* tz) {
   switch (nq) {

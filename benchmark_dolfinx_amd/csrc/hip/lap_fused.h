@@ -173,7 +173,6 @@ template <> struct TileFor<9> { static constexpr int TY = 1, TZ = 3; };
 
 // Packed 1D tables + quadrature, passed by value in the kernarg segment
 // (constant address space: wave-uniform reads become scalar loads).
-constexpr int kFusedTabMax = 2 * 9 * 12 + 9 * 8 + 8 * 12;  // TAB for nd=8, nq=9 (f32 pitch)
 template <typename T>
 struct FusedTables {
   T tab[kFusedTabMax];

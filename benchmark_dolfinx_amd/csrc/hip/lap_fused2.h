@@ -72,6 +72,7 @@ struct Fused2Args {
   int bcx_lo, bcx_hi;            // local index of the global boundary plane, -1 if none
   int bcy_lo, bcy_hi, bcz_lo, bcz_hi;
   int nty, ntz;
+  int ty0, tz0, rwz, nblk;       // tile rectangle of this launch: [ty0, ty0 + nblk / rwz) x [tz0, tz0 + rwz)
   int beta_num, beta_den;        // CG: beta = scal[num] / scal[den]; num < 0 -> 0
   int xa_num, xa_den;            // CG: alpha_prev = scal[num] / scal[den]; num < 0 -> no x update
   T kappa;
@@ -118,7 +119,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   const int nblk = gridDim.x, ob = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
-  const int ty = bid / A.ntz, tz = bid % A.ntz;
+  const int ty = A.ty0 + bid / A.rwz, tz = A.tz0 + bid % A.rwz;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
   const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
   const int ncx = A.ncx;
@@ -693,7 +694,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
-    if (tid == 0) A.partials[blockIdx.x] = t;
+    if (tid == 0) A.partials[ty * A.ntz + tz] = t;  // tile-indexed: launch-split invariant
   }
 }
 
@@ -704,7 +705,7 @@ template <typename T, int ND, int NQ, int MODE>
 int launch_fused2(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
   using TF = TileFor<NQ>;
   using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
-  const int nblk = a.nty * a.ntz;
+  const int nblk = a.nblk;
   if (nblk <= 0) return 0;
   if (affine)
     lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
@@ -746,6 +747,27 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
   a.bcz_hi = hi(2);
   a.nty = nty;
   a.ntz = ntz;
+  a.ty0 = a.tz0 = 0;
+  a.rwz = ntz;
+  a.nblk = nty * ntz;
+  return 0;
+}
+
+// Restrict a launch to the tile rectangle rect = {ty0, ty1, tz0, tz1} (host
+// memory; null = every tile).  The runtime splits one operator apply into
+// disjoint rectangles to overlap the halo exchange with the tiles that do not
+// touch a ghost plane; p.Ap partials are tile-indexed, so the reduction is
+// identical for any split.
+template <typename T>
+inline int fused_set_rect(Fused2Args<T>& a, const int* rect) {
+  if (!rect) return 0;
+  const int ty0 = rect[0], ty1 = rect[1], tz0 = rect[2], tz1 = rect[3];
+  if (ty0 < 0 || tz0 < 0 || ty1 > a.nty || tz1 > a.ntz || ty1 < ty0 || tz1 < tz0)
+    return static_cast<int>(hipErrorInvalidValue);
+  a.ty0 = ty0;
+  a.tz0 = tz0;
+  a.rwz = tz1 > tz0 ? tz1 - tz0 : 1;
+  a.nblk = (ty1 - ty0) * (tz1 - tz0);
   return 0;
 }
 
@@ -756,9 +778,10 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
       const T* u, const T* pold, T* pnew, T* x, T* y, T* yb, T* zb, T* cb,         \
       const T* xv, const T* kc, const T* tabs, double kappa, const double* scal,   \
       double* partials, int beta_num, int beta_den, int xa_num, int xa_den,        \
-      int nty, int ntz, hipStream_t st) {                                          \
+      int nty, int ntz, const int* rect, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
-    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));       \
+    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \

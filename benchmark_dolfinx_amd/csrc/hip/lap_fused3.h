@@ -111,7 +111,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   const int nblk = gridDim.x, ob = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
-  const int ty = bid / A.ntz, tz = bid % A.ntz;
+  const int ty = A.ty0 + bid / A.rwz, tz = A.tz0 + bid % A.rwz;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
   const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
   const int ncx = A.ncx;
@@ -708,7 +708,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
-    if (tid == 0) A.partials[blockIdx.x] = t;
+    if (tid == 0) A.partials[ty * A.ntz + tz] = t;  // tile-indexed: launch-split invariant
   }
 }
 
@@ -719,7 +719,7 @@ template <typename T, int ND, int NQ, int MODE>
 int launch_fused3(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
   using TF = TileFor<NQ>;
   using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
-  const int nblk = a.nty * a.ntz;
+  const int nblk = a.nblk;
   if (nblk <= 0) return 0;
   if (affine)
     lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
@@ -735,9 +735,10 @@ int launch_fused3(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, 
       const T* u, const T* pold, T* pnew, T* x, T* y, T* yb, T* zb, T* cb,         \
       const T* xv, const T* kc, const T* tabs, double kappa, const double* scal,   \
       double* partials, int beta_num, int beta_den, int xa_num, int xa_den,        \
-      int nty, int ntz, hipStream_t st) {                                          \
+      int nty, int ntz, const int* rect, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
-    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));       \
+    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \

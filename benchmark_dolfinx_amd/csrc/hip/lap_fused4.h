@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   const int nblk = gridDim.x, ob = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
-  const int ty = bid / A.ntz, tz = bid % A.ntz;
+  const int ty = A.ty0 + bid / A.rwz, tz = A.tz0 + bid % A.rwz;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
   const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
   const int ncx = A.ncx;
@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
-    if (tid == 0) A.partials[blockIdx.x] = t;
+    if (tid == 0) A.partials[ty * A.ntz + tz] = t;  // tile-indexed: launch-split invariant
   }
 }
 
@@ -594,7 +594,7 @@ inline int pack_tables4(int nd, int nq, const double* phi0, const double* Dd, co
 template <int MODE>
 int launch_fused4(const Fused2Args<double>& a, const FusedTables<double>& tb, hipStream_t st) {
   constexpr int TY = BDX_F4_TY, TZ = BDX_F4_TZ;
-  const int nblk = a.nty * a.ntz;
+  const int nblk = a.nblk;
   if (nblk <= 0) return 0;
   lap_fused4_kernel<TY, TZ, MODE><<<nblk, TY * TZ * 16, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());

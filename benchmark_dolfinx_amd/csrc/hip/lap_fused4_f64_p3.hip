@@ -6,7 +6,7 @@ extern "C" int bdx_fused4_apply_f64_p3(
     const double* u, const double* pold, double* pnew, double* x, double* y, double* yb,
     double* zb, double* cb, const double* xv, const double* kc, const double* tabs, double kappa,
     const double* scal, double* partials, int beta_num, int beta_den, int xa_num, int xa_den,
-    int nty, int ntz, hipStream_t st) {
+    int nty, int ntz, const int* rect, hipStream_t st) {
   (void)wts;
   (void)qpts;
   (void)nq;
@@ -14,6 +14,7 @@ extern "C" int bdx_fused4_apply_f64_p3(
   if (!affine_ok || !tabs) return static_cast<int>(hipErrorInvalidValue);
   Fused2Args<double> a;
   BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));
+  BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));
   a.u = u;
   a.pold = pold;
   a.pnew = pnew;
@@ -48,3 +49,6 @@ extern "C" int bdx_fused4_tile(int* ty, int* tz) {
   *tz = BDX_F4_TZ;
   return 0;
 }
+
+// Timing-only phase drops compiled into this TU (0 in a valid build).
+extern "C" int bdx_drop_flags_f4() { return BDX_F4_DROP; }

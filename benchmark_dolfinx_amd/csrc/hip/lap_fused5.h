@@ -27,7 +27,9 @@
 // wave at ND = 5 / 4, so the passes exchange data only inside a wave:
 // wave-local syncs, in-place rewrites of one per-wave buffer, two workgroup
 // barriers per cell layer (gather and staging).  The 1D matrices are
-// wave-uniform kernarg values (scalar loads).  On axis-aligned boxes
+// wave-uniform scalar loads from a device buffer that each operator owns
+// (allocated at construction, passed by pointer: a captured hipGraph keeps
+// reading its own operator's tables).  On axis-aligned boxes
 // (diagonal Jacobians, the benchmark mesh; exact host check) the 2-array
 // instance runs: 7 ND^2 FMAs per lane and cell.
 //
@@ -36,9 +38,6 @@
 // x update, Dirichlet identity rows, p.Ap partials as element dots) and the
 // atomic-free gather with tile-interface buffers -- is fused4's.
 #pragma once
-#include <cstring>
-#include <mutex>
-
 #include "lap_fused2.h"
 
 #ifndef BDX_F5_WAVES
@@ -50,7 +49,7 @@
 #define BDX_F5_DROP 0
 #endif
 
-// kernarg table layout: M, K, C, C^T as 8 x 8 row-major blocks
+// table layout: M, K, C, C^T as 8 x 8 row-major blocks
 constexpr int kF5Stride = 8;
 constexpr int kF5Tab = 4 * 64;
 static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
@@ -126,7 +125,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
   const int nblk = gridDim.x, ob = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
-  const int ty = bid / A.ntz, tz = bid % A.ntz;
+  const int ty = A.ty0 + bid / A.rwz, tz = A.tz0 + bid % A.rwz;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
   const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
   const int ncx = A.ncx;
@@ -594,7 +593,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
-    if (tid == 0) A.partials[blockIdx.x] = t;
+    if (tid == 0) A.partials[ty * A.ntz + tz] = t;  // tile-indexed: launch-split invariant
   }
 }
 
@@ -626,7 +625,7 @@ inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, co
 // boxes (diagonal Jacobians: the 2-array instance)
 template <typename T, int ND, int MODE>
 int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStream_t st) {
-  const int nblk = a.nty * a.ntz;
+  const int nblk = a.nblk;
   if (nblk <= 0) return 0;
   if (affine_ok == 2)
     lap_fused5_kernel<T, ND, 2, MODE><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
@@ -635,58 +634,20 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
   return static_cast<int>(hipGetLastError());
 }
 
-// Device copy of the host tables in a per-TU __device__ array: uploaded when
-// the content differs from what the current device holds (a new problem),
-// never inside a stream capture (the first, uncaptured launches of a
-// configuration upload; replays see the same content).  The device is
-// synchronised before an overwrite so no queued kernel reads a half-updated
-// table.  Returns the device address of the array, or null on error.
-template <typename T>
-inline const T* f5_tables_on_device(T* sym_addr_holder, const void* sym, const T* host,
-                                    hipStream_t st, int* err) {
-  static std::mutex mu;
-  static T shadow[16][kFusedTabMax];
-  static bool valid[16] = {};
-  (void)sym_addr_holder;
-  int dev = 0;
-  *err = static_cast<int>(hipGetDevice(&dev));
-  if (*err || dev < 0 || dev >= 16) {
-    if (!*err) *err = static_cast<int>(hipErrorInvalidDevice);
-    return nullptr;
-  }
-  std::lock_guard<std::mutex> lk(mu);
-  if (!valid[dev] || std::memcmp(shadow[dev], host, sizeof(T) * kFusedTabMax) != 0) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if ((*err = static_cast<int>(hipStreamIsCapturing(st, &cs)))) return nullptr;
-    if (cs != hipStreamCaptureStatusNone) {
-      *err = static_cast<int>(hipErrorStreamCaptureUnsupported);
-      return nullptr;
-    }
-    if ((*err = static_cast<int>(hipDeviceSynchronize()))) return nullptr;
-    if ((*err = static_cast<int>(hipMemcpyToSymbol(sym, host, sizeof(T) * kFusedTabMax))))
-      return nullptr;
-    std::memcpy(shadow[dev], host, sizeof(T) * kFusedTabMax);
-    valid[dev] = true;
-  }
-  void* p = nullptr;
-  if ((*err = static_cast<int>(hipGetSymbolAddress(&p, sym)))) return nullptr;
-  return static_cast<const T*>(p);
-}
-
 #define BDX_FUSED5_TU(T, SUF, PP)                                                   \
-  static __device__ T g_f5tab[kFusedTabMax];                                       \
   extern "C" int bdx_fused5_apply_##SUF##_p##PP(                                   \
       int mode, int affine_ok, const int64_t* latd, int nq, const double* wts,     \
       const double* qpts, const T* u, const T* pold, T* pnew, T* x, T* y, T* yb,   \
       T* zb, T* cb, const T* xv, const T* kc, const T* tabs, double kappa,         \
       const double* scal, double* partials, int beta_num, int beta_den,            \
-      int xa_num, int xa_den, int nty, int ntz, hipStream_t st) {                  \
+      int xa_num, int xa_den, int nty, int ntz, const int* rect, hipStream_t st) {                  \
     (void)wts;                                                                     \
     (void)qpts;                                                                    \
     (void)nq;                                                                      \
     if (!affine_ok || !tabs) return static_cast<int>(hipErrorInvalidValue);        \
     Fused2Args<T> a;                                                               \
-    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));       \
+    BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \
@@ -704,9 +665,7 @@ inline const T* f5_tables_on_device(T* sym_addr_holder, const void* sym, const T
     a.xa_num = xa_num;                                                             \
     a.xa_den = xa_den;                                                             \
     a.kappa = static_cast<T>(kappa);                                               \
-    int err = 0;                                                                   \
-    const T* tabd = f5_tables_on_device<T>(nullptr, HIP_SYMBOL(g_f5tab), tabs, st, &err); \
-    if (!tabd) return err ? err : static_cast<int>(hipErrorInvalidValue);          \
+    const T* tabd = tabs; /* device pointer: the operator's own table buffer */   \
     return mode == kFusedCG ? launch_fused5<T, PP + 1, kFusedCG>(affine_ok, a, tabd, st) \
                             : launch_fused5<T, PP + 1, kFusedAction>(affine_ok, a, tabd, st); \
   }                                                                                \
@@ -715,6 +674,7 @@ inline const T* f5_tables_on_device(T* sym_addr_holder, const void* sym, const T
                                                   T* out) {                        \
     return pack_tables5<T>(nd, nq, phi0, Dd, wts, out);                            \
   }                                                                                \
+  extern "C" int bdx_drop_flags_f5_##SUF##_p##PP() { return BDX_F5_DROP; }          \
   extern "C" int bdx_fused5_tile_p##PP##_##SUF(int affine_ok, int* ty, int* tz) {  \
     *ty = affine_ok == 2 ? F5Tile<PP + 1, 2>::TY : F5Tile<PP + 1, 4>::TY;          \
     *tz = affine_ok == 2 ? F5Tile<PP + 1, 2>::TZ : F5Tile<PP + 1, 4>::TZ;          \

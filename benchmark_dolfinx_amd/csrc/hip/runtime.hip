@@ -2,33 +2,55 @@
 //
 // The reference drives its CG from C++ (src/cg.hpp:89-169) over GPU-aware MPI
 // with host round trips per dot product and two halo scatters per iteration
-// (SURVEY.md quirks Q2/Q3).  This runtime owns one rank's iteration:
+// (SURVEY.md quirks Q2/Q3), overlapping the forward scatter with the
+// interior-cell kernel (src/laplacian.hpp:281-349).  This runtime owns one
+// rank's iteration on two HIP streams, every scalar device-resident:
 //
-//   [halo fwd of r]  fused2/3(CG)  [ghost finalize + halo rev of y]
-//   reduce(p.Ap) -> all-reduce(device scalar) -> r update (+ r.r) -> all-reduce
+//   compute stream                         comm stream
+//   --------------                         -----------
+//   fused op, interior tiles A      ||     pack r faces -> RCCL send/recv -> unpack ghosts
+//   fused op, ghost-touching tiles  (after the forward exchange)
+//   ghost-plane finalize
+//   fused op, interior tiles B      ||     pack y ghosts -> RCCL send/recv
+//   unpack-add y faces (after the reverse exchange)
+//   reduce(p.Ap) -> all-reduce -> r update (+ r.r) -> all-reduce
 //
-// on one HIP stream, with every scalar device-resident, the halo as grouped
-// RCCL point-to-point sends/receives with the <= 7 (faces/edges/corner)
-// neighbours over xGMI, and the steady-state iterations (two parities: the
-// p buffers and the r.r slots ping-pong) captured once into hipGraphs and
-// replayed.  A second transport runs R ranks as threads of one process on one
-// GPU (host barriers + device copies) so the multi-rank orchestration is
-// testable on a single-GPU box; graphs are used with RCCL or a single rank.
+// The tile split needs an unsplit march axis (x): the partition keeps x whole
+// on the GPU platform (fem/mesh.py partition_grid), so only the last (y, z)
+// tile row / column touches a ghost plane and every other tile can run while
+// the halo is in flight; both exchanges are hidden.  Otherwise (x split, one
+// rank) the iteration runs serially on the compute stream.  Halos are
+// grouped RCCL point-to-point sends/receives with the <= 7 neighbours over
+// xGMI; the steady-state iterations (two parities: the p buffers and the r.r
+// slots ping-pong) are captured once into hipGraphs (fork/join over the two
+// streams) and replayed.
+//
+// Failure containment: every blocking RCCL call and host wait runs inside a
+// bdx::Watchdog scope (csrc/include/bdx_watchdog.h); past the deadline
+// (BDX_RCCL_TIMEOUT_S, default 300 s) or on an asynchronous communicator
+// error the communicator is aborted and the call returns an error that
+// Python raises.  A second transport runs R ranks as threads of one process
+// on one GPU (host barriers + device copies) so the multi-rank orchestration
+// is testable on a single-GPU box.
 //
 // Python (solvers/native.py) builds the problem, runs the CG prologue
 // (r0 = b - A x0, rho0) and hands the device buffers to this runtime.
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "bdx_common.h"
+#include "bdx_watchdog.h"
 
 extern "C" {
 int bdx_box_copy_f64(int, double*, int64_t, int64_t, const int64_t*, int, int64_t, double*,
@@ -52,14 +74,14 @@ int bdx_xflush_f32(const int64_t*, const int64_t*, float*, const float*, const d
                    int, hipStream_t);
 }
 
-// The fused2/3 operator entry points (lap_fused{2,3}_<suf>_p<P>.hip); weak so
-// that experiment builds holding a subset of the operator TUs still load
-// (a missing instance resolves to null and bdx_rt_create refuses it).
+// The fused2..5 operator entry points (lap_fused{2,3,4,5}_<suf>_p<P>.hip);
+// weak so that experiment builds holding a subset of the operator TUs still
+// load (a missing instance resolves to null and bdx_rt_create refuses it).
 #define BDX_DECL_APPLY(V, T, SUF, PP)                                                        \
   extern "C" __attribute__((weak)) int bdx_fused##V##_apply_##SUF##_p##PP(                  \
       int, int, const int64_t*, int, const double*, const double*, const T*, const T*, T*, \
       T*, T*, T*, T*, T*, const T*, const T*, const T*, double, const double*, double*, int, \
-      int, int, int, int, int, hipStream_t);
+      int, int, int, int, int, const int*, hipStream_t);
 #define BDX_DECL_ALL(V)                                                                    \
   BDX_DECL_APPLY(V, double, f64, 1) BDX_DECL_APPLY(V, double, f64, 2)                      \
   BDX_DECL_APPLY(V, double, f64, 3) BDX_DECL_APPLY(V, double, f64, 4)                      \
@@ -82,7 +104,8 @@ namespace {
 template <typename T>
 using ApplyFn = int (*)(int, int, const int64_t*, int, const double*, const double*, const T*,
                         const T*, T*, T*, T*, T*, T*, T*, const T*, const T*, const T*, double,
-                        const double*, double*, int, int, int, int, int, int, hipStream_t);
+                        const double*, double*, int, int, int, int, int, int, const int*,
+                        hipStream_t);
 
 template <typename T>
 ApplyFn<T> apply_fn(int version, int P);
@@ -109,6 +132,10 @@ ApplyFn<float> apply_fn<float>(int version, int P) {
   return nullptr;
 }
 
+// Error codes returned to Python (besides hipError_t values).
+constexpr int kErrAborted = -20;   // the watchdog aborted the communicator
+constexpr int kErrNotConnected = -21;
+
 // ------------------------------------------------------------------ transports
 struct Transport {
   virtual ~Transport() = default;
@@ -120,35 +147,128 @@ struct Transport {
                        int esize, hipStream_t st) = 0;
   virtual int allreduce_sum(double* dev, int n, hipStream_t st) = 0;
   virtual bool capturable() const = 0;
+  virtual int ranks() const = 0;
+  // Host wait for `ev` (the end of queued work that may contain
+  // communication), bounded by the transport's deadline.
+  virtual int wait(hipEvent_t ev) { return static_cast<int>(hipEventSynchronize(ev)); }
+  virtual bool aborted() const { return false; }
 };
 
+double rccl_timeout_s() {
+  const char* e = std::getenv("BDX_RCCL_TIMEOUT_S");
+  return e ? std::atof(e) : 300.0;
+}
+
 struct RcclTransport final : Transport {
-  ncclComm_t comm = nullptr;
+  std::atomic<ncclComm_t> comm{nullptr};
   int nranks = 1;
-  ~RcclTransport() override {
-    if (comm) ncclCommDestroy(comm);
+  std::atomic<bool> was_aborted{false};
+  std::unique_ptr<bdx::Watchdog> wd;
+
+  RcclTransport() {
+    wd = std::make_unique<bdx::Watchdog>(
+        rccl_timeout_s(),
+        [this] {
+          ncclComm_t c = comm.load();
+          if (!c || was_aborted.load()) return false;
+          ncclResult_t e = ncclSuccess;
+          if (ncclCommGetAsyncError(c, &e) != ncclSuccess) return true;
+          return e != ncclSuccess && e != ncclInProgress;
+        },
+        [this] {
+          ncclComm_t c = comm.load();
+          if (!c) {
+            // still inside ncclCommInitRank: nothing to abort, fail fast
+            std::fprintf(stderr,
+                         "[bdx] RCCL communicator init exceeded %.0f s; a peer never joined. "
+                         "Exiting.\n",
+                         wd->timeout_s());
+            std::fflush(stderr);
+            std::_Exit(124);
+          }
+          std::fprintf(stderr, "[bdx] RCCL %s; aborting the communicator\n",
+                       wd->reason() == 1 ? "call exceeded the deadline" : "asynchronous error");
+          std::fflush(stderr);
+          was_aborted.store(true);
+          ncclCommAbort(c);
+        });
   }
+  ~RcclTransport() override {
+    if (wd) wd->stop();
+    ncclComm_t c = comm.load();
+    if (c && !was_aborted.load()) ncclCommDestroy(c);
+  }
+  int connect(const ncclUniqueId& id, int n, int rank) {
+    nranks = n;
+    wd->start();
+    bdx::Watchdog::Busy b(wd.get());
+    ncclComm_t c = nullptr;
+    if (ncclCommInitRank(&c, n, id, rank) != ncclSuccess) return -1;
+    comm.store(c);
+    return 0;
+  }
+  bool aborted() const override { return was_aborted.load(); }
   int exchange(const void* sbuf, const std::vector<int64_t>& scnt,
                const std::vector<int64_t>& soff, void* rbuf, const std::vector<int64_t>& rcnt,
                const std::vector<int64_t>& roff, int esize, hipStream_t st) override {
+    ncclComm_t c = comm.load();
+    if (!c) return kErrNotConnected;
+    if (was_aborted.load()) return kErrAborted;
+    bdx::Watchdog::Busy b(wd.get());
     const ncclDataType_t dt = esize == 8 ? ncclFloat64 : ncclFloat32;
     if (ncclGroupStart() != ncclSuccess) return -1;
     for (int p = 0; p < nranks; ++p) {
       if (scnt[p] > 0 &&
-          ncclSend(static_cast<const char*>(sbuf) + soff[p] * esize, scnt[p], dt, p, comm, st) !=
+          ncclSend(static_cast<const char*>(sbuf) + soff[p] * esize, scnt[p], dt, p, c, st) !=
               ncclSuccess)
         return -2;
       if (rcnt[p] > 0 &&
-          ncclRecv(static_cast<char*>(rbuf) + roff[p] * esize, rcnt[p], dt, p, comm, st) !=
+          ncclRecv(static_cast<char*>(rbuf) + roff[p] * esize, rcnt[p], dt, p, c, st) !=
               ncclSuccess)
         return -3;
     }
-    return ncclGroupEnd() == ncclSuccess ? 0 : -4;
+    const ncclResult_t e = ncclGroupEnd();
+    if (was_aborted.load()) return kErrAborted;
+    return e == ncclSuccess ? 0 : -4;
   }
   int allreduce_sum(double* dev, int n, hipStream_t st) override {
-    return ncclAllReduce(dev, dev, n, ncclFloat64, ncclSum, comm, st) == ncclSuccess ? 0 : -5;
+    ncclComm_t c = comm.load();
+    if (!c) return kErrNotConnected;
+    if (was_aborted.load()) return kErrAborted;
+    bdx::Watchdog::Busy b(wd.get());
+    const ncclResult_t e = ncclAllReduce(dev, dev, n, ncclFloat64, ncclSum, c, st);
+    if (was_aborted.load()) return kErrAborted;
+    return e == ncclSuccess ? 0 : -5;
+  }
+  int wait(hipEvent_t ev) override {
+    bdx::Watchdog::Busy b(wd.get());
+    for (;;) {
+      const hipError_t e = hipEventQuery(ev);
+      if (e == hipSuccess) return 0;
+      if (e != hipErrorNotReady) return static_cast<int>(e);
+      if (was_aborted.load()) return kErrAborted;
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
   }
   bool capturable() const override { return true; }
+  int ranks() const override {
+    ncclComm_t c = comm.load();
+    int n = 0;
+    if (!c || ncclCommCount(c, &n) != ncclSuccess) return -1;
+    return n;
+  }
+};
+
+// Single rank: no communication at all.
+struct NoTransport final : Transport {
+  int exchange(const void*, const std::vector<int64_t>&, const std::vector<int64_t>&, void*,
+               const std::vector<int64_t>&, const std::vector<int64_t>&, int,
+               hipStream_t) override {
+    return 0;
+  }
+  int allreduce_sum(double*, int, hipStream_t) override { return 0; }
+  bool capturable() const override { return true; }
+  int ranks() const override { return 1; }
 };
 
 // R ranks = R threads of one process on one device (tests): host barriers,
@@ -212,10 +332,28 @@ struct ThreadTransport final : Transport {
     return 0;
   }
   bool capturable() const override { return false; }
+  int ranks() const override { return g->size; }
 };
 
 // ------------------------------------------------------------------ the CG loop
 constexpr int kRR0 = 0, kRR1 = 1, kPAP = 2;
+
+// Phase marks of one iteration (bdx_rt_profile).  In the serial schedule the
+// marks that belong to the split schedule coincide with their neighbours.
+enum Mark {
+  kMStart = 0,   // compute stream: iteration start
+  kMFwdBeg,      // comm stream: forward exchange start
+  kMFwdEnd,      // comm stream: ghost planes of r unpacked
+  kMOpA,         // compute: interior tiles A done (serial: the whole operator)
+  kMBnd,         // compute: ghost-touching tiles + ghost finalize done
+  kMRevBeg,      // comm: reverse exchange start
+  kMRevEnd,      // comm: reverse exchange done (serial: + unpack-add)
+  kMOpB,         // compute: interior tiles B done
+  kMPap,         // compute: unpack-add + reduce + all-reduce(p.Ap) done
+  kMUpd,         // compute: r update (+ r.r) done
+  kMEnd,         // compute: all-reduce(r.r) done
+  kNMarks
+};
 
 struct RtConfig {
   int64_t latd[17];
@@ -230,13 +368,15 @@ struct CGRuntime {
   RtConfig cfg;
   std::unique_ptr<Transport> tr;
   int nranks = 1;
-  // own non-blocking stream (graph capture is not allowed on the legacy
+  // own non-blocking streams (graph capture is not allowed on the legacy
   // default stream torch may be using); ordered against the caller's stream
   // `ext` with events at the start and end of every iterate()
-  hipStream_t st = nullptr, ext = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipStream_t st = nullptr, cs = nullptr, ext = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_fwd = nullptr,
+             ev_bnd = nullptr, ev_rev = nullptr;
   ApplyFn<T> apply = nullptr;
-  std::vector<T> tabs;
+  std::vector<T> tabs_host;
+  const T* tabs = nullptr;  // host copy (fused2-4: kernarg tables) or device buffer (fused5)
   T *x, *r, *pa, *pb, *y, *yb, *zb, *cb;
   const T* xv;
   const T* kc = nullptr;
@@ -248,30 +388,54 @@ struct CGRuntime {
   int nface_boxes = 0, nghost_boxes = 0;
   int64_t face_total = 0, ghost_total = 0;
   std::vector<int64_t> face_cnt, face_off, ghost_cnt, ghost_off;
+  // overlapped schedule: tile rectangles {ty0, ty1, tz0, tz1}
+  bool split = false;
+  int rect_a[4], rect_b[4], rect_r1[4], rect_r2[4];
+  // phase profiling (eager iterations only)
+  bool prof = false;
+  hipEvent_t pev[kNMarks] = {};
   // state
   long it = 0;
   bool x_lag = false;
   bool use_graph = true, graph_ok[2] = {false, false};
   hipGraphExec_t graph[2] = {nullptr, nullptr};
 
-  int box_copy(int mode, T* vec, const int64_t* boxes, int nb, int64_t total, T* buf) {
+  void mark(int id, hipStream_t s) {
+    if (prof) (void)hipEventRecord(pev[id], s);
+  }
+  int box_copy(int mode, T* vec, const int64_t* boxes, int nb, int64_t total, T* buf,
+               hipStream_t s) {
     const BdxLattice L = BdxLattice::from(cfg.latd);
     if constexpr (sizeof(T) == 8)
-      return bdx_box_copy_f64(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, st);
+      return bdx_box_copy_f64(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, s);
     else
-      return bdx_box_copy_f32(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, st);
+      return bdx_box_copy_f32(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, s);
   }
-  int halo_forward(T* v) {
-    BDX_CHECK(static_cast<hipError_t>(box_copy(0, v, face_boxes, nface_boxes, face_total, hbuf_a)));
-    int rc = tr->exchange(hbuf_a, face_cnt, face_off, hbuf_b, ghost_cnt, ghost_off, sizeof(T), st);
-    if (rc) return rc;
-    return box_copy(1, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_b);
+  // forward: owned lower faces of v -> peers' ghost planes (pack, exchange, unpack)
+  int halo_forward(T* v, hipStream_t s) {
+    int rc = box_copy(0, v, face_boxes, nface_boxes, face_total, hbuf_a, s);
+    if (rc || (rc = tr->exchange(hbuf_a, face_cnt, face_off, hbuf_b, ghost_cnt, ghost_off,
+                                 sizeof(T), s)))
+      return rc;
+    return box_copy(1, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_b, s);
   }
-  int halo_reverse(T* v) {
-    BDX_CHECK(static_cast<hipError_t>(box_copy(0, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_a)));
-    int rc = tr->exchange(hbuf_a, ghost_cnt, ghost_off, hbuf_b, face_cnt, face_off, sizeof(T), st);
+  // reverse, first half: ghost-plane partial sums of v -> peers (pack, exchange)
+  int halo_reverse_send(T* v, hipStream_t s) {
+    const int rc = box_copy(0, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_a, s);
     if (rc) return rc;
-    return box_copy(2, v, face_boxes, nface_boxes, face_total, hbuf_b);
+    return tr->exchange(hbuf_a, ghost_cnt, ghost_off, hbuf_b, face_cnt, face_off, sizeof(T), s);
+  }
+  // reverse, second half: add the received sums into the owned lower faces
+  int halo_reverse_add(T* v, hipStream_t s) {
+    return box_copy(2, v, face_boxes, nface_boxes, face_total, hbuf_b, s);
+  }
+  int finalize_ghost(hipStream_t s) {
+    if constexpr (sizeof(T) == 8)
+      return bdx_fused_finalize_f64(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
+                                    s);
+    else
+      return bdx_fused_finalize_f32(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
+                                    s);
   }
 
   // One CG iteration with explicit parity / flags (stream-ordered, no sync).
@@ -279,22 +443,53 @@ struct CGRuntime {
     const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
     T* pold = (k % 2 == 0) ? pa : pb;
     T* pnew = (k % 2 == 0) ? pb : pa;
+    auto op = [&](const int* rect, hipStream_t s) {
+      return apply(1, cfg.affine, cfg.latd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
+                   pnew, x, y, yb, zb, cb, xv, kc, tabs, cfg.kappa, scal, partials,
+                   first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1,
+                   cfg.nty, cfg.ntz, rect, s);
+    };
     int rc;
-    if (halo && (rc = halo_forward(r))) return rc;
-    rc = apply(1, cfg.affine, cfg.latd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold, pnew,
-               x, y, yb, zb, cb, xv, kc, tabs.data(), cfg.kappa, scal, partials,
-               first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1, cfg.nty,
-               cfg.ntz, st);
-    if (rc) return rc;
-    if (halo) {
-      if constexpr (sizeof(T) == 8)
-        rc = bdx_fused_finalize_f64(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1, st);
-      else
-        rc = bdx_fused_finalize_f32(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1, st);
-      if (rc || (rc = halo_reverse(y))) return rc;
+    mark(kMStart, st);
+    if (split) {
+      BDX_CHECK(hipEventRecord(ev_fork, st));
+      BDX_CHECK(hipStreamWaitEvent(cs, ev_fork, 0));
+      mark(kMFwdBeg, cs);
+      if ((rc = halo_forward(r, cs))) return rc;
+      BDX_CHECK(hipEventRecord(ev_fwd, cs));
+      mark(kMFwdEnd, cs);
+      if ((rc = op(rect_a, st))) return rc;
+      mark(kMOpA, st);
+      BDX_CHECK(hipStreamWaitEvent(st, ev_fwd, 0));
+      if ((rc = op(rect_r1, st)) || (rc = op(rect_r2, st)) || (rc = finalize_ghost(st)))
+        return rc;
+      BDX_CHECK(hipEventRecord(ev_bnd, st));
+      mark(kMBnd, st);
+      BDX_CHECK(hipStreamWaitEvent(cs, ev_bnd, 0));
+      mark(kMRevBeg, cs);
+      if ((rc = halo_reverse_send(y, cs))) return rc;
+      BDX_CHECK(hipEventRecord(ev_rev, cs));
+      mark(kMRevEnd, cs);
+      if ((rc = op(rect_b, st))) return rc;
+      mark(kMOpB, st);
+      BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
+      if ((rc = halo_reverse_add(y, st))) return rc;
+    } else {
+      mark(kMFwdBeg, st);
+      if (halo && (rc = halo_forward(r, st))) return rc;
+      mark(kMFwdEnd, st);
+      if ((rc = op(nullptr, st))) return rc;
+      mark(kMOpA, st);
+      if (halo && (rc = finalize_ghost(st))) return rc;
+      mark(kMBnd, st);
+      mark(kMRevBeg, st);
+      if (halo && ((rc = halo_reverse_send(y, st)) || (rc = halo_reverse_add(y, st)))) return rc;
+      mark(kMRevEnd, st);
+      mark(kMOpB, st);
     }
     if ((rc = bdx_reduce_partials(partials, cfg.nblocks, scal, kPAP, st))) return rc;
     if (nranks > 1 && (rc = tr->allreduce_sum(scal + kPAP, 1, st))) return rc;
+    mark(kMPap, st);
     if constexpr (sizeof(T) == 8)
       rc = bdx_cg_update_iface_f64(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
                                    cfg.sz, scal, cur, kPAP, nxt, upart, st);
@@ -302,7 +497,9 @@ struct CGRuntime {
       rc = bdx_cg_update_iface_f32(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
                                    cfg.sz, scal, cur, kPAP, nxt, upart, st);
     if (rc) return rc;
+    mark(kMUpd, st);
     if (nranks > 1 && (rc = tr->allreduce_sum(scal + nxt, 1, st))) return rc;
+    mark(kMEnd, st);
     return 0;
   }
 
@@ -326,7 +523,16 @@ struct CGRuntime {
     return ok;
   }
 
+  void drop_graphs() {
+    for (int i = 0; i < 2; ++i) {
+      if (graph[i]) hipGraphExecDestroy(graph[i]);
+      graph[i] = nullptr;
+      graph_ok[i] = false;
+    }
+  }
+
   int iterate(long n) {
+    if (tr->aborted()) return kErrAborted;
     BDX_CHECK(hipEventRecord(ev_in, ext));
     BDX_CHECK(hipStreamWaitEvent(st, ev_in, 0));
     int rc = iterate_on_stream(n);
@@ -339,13 +545,12 @@ struct CGRuntime {
     for (long i = 0; i < n; ++i) {
       const bool first = (it == 0);
       const int par = static_cast<int>(it % 2);
-      if (!first && x_lag && use_graph && tr->capturable()) {
-        if (!graph_ok[par]) {
-          graph_ok[par] = capture(par);
-          if (!graph_ok[par]) use_graph = false;  // fall back to eager launches
-        }
+      const bool steady = !first && x_lag && !prof;
+      if (steady && use_graph && tr->capturable() && !graph_ok[par]) {
+        graph_ok[par] = capture(par);
+        if (!graph_ok[par]) use_graph = false;  // fall back to eager launches
       }
-      if (!first && x_lag && use_graph && graph_ok[par]) {
+      if (steady && use_graph && graph_ok[par]) {
         BDX_CHECK(hipGraphLaunch(graph[par], st));
       } else {
         const int rc = step(it, first, x_lag);
@@ -368,12 +573,57 @@ struct CGRuntime {
       return bdx_xflush_f32(cfg.latd, cfg.own, x, plast, scal, last, kPAP, st);
   }
 
+  // n eager iterations with timing events between the phases; out[i] = mean
+  // ms of interval i (see bdx_rt_profile for the list).
+  int profile(long n, double* out, int nout) {
+    if (nout < kNPhases) return static_cast<int>(hipErrorInvalidValue);
+    for (int i = 0; i < kNMarks; ++i)
+      if (!pev[i]) BDX_CHECK(hipEventCreate(&pev[i]));
+    for (int i = 0; i < nout; ++i) out[i] = 0.0;
+    BDX_CHECK(hipEventRecord(ev_in, ext));
+    BDX_CHECK(hipStreamWaitEvent(st, ev_in, 0));
+    prof = true;
+    int rc = 0;
+    for (long i = 0; i < n && !rc; ++i) {
+      const bool first = (it == 0);
+      rc = step(it, first, x_lag);
+      if (rc) break;
+      x_lag = true;
+      ++it;
+      BDX_CHECK(hipEventRecord(ev_out, st));
+      if ((rc = tr->wait(ev_out))) break;
+      auto dt = [&](int a, int b) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, pev[a], pev[b]);
+        return static_cast<double>(ms);
+      };
+      out[0] += dt(kMFwdBeg, kMFwdEnd);
+      out[1] += dt(kMStart, kMOpA);
+      out[2] += dt(kMOpA, kMBnd);
+      out[3] += dt(kMRevBeg, kMRevEnd);
+      out[4] += dt(kMBnd, kMOpB);
+      out[5] += dt(kMOpB, kMPap);
+      out[6] += dt(kMPap, kMUpd);
+      out[7] += dt(kMUpd, kMEnd);
+      out[8] += dt(kMStart, kMEnd);
+    }
+    prof = false;
+    if (!rc) rc = flush();
+    BDX_CHECK(hipEventRecord(ev_out, st));
+    BDX_CHECK(hipStreamWaitEvent(ext, ev_out, 0));
+    for (int i = 0; i < kNPhases && n > 0; ++i) out[i] /= static_cast<double>(n);
+    return rc;
+  }
+  static constexpr int kNPhases = 9;
+
   ~CGRuntime() {
-    for (auto& g : graph)
-      if (g) hipGraphExecDestroy(g);
-    if (ev_in) hipEventDestroy(ev_in);
-    if (ev_out) hipEventDestroy(ev_out);
+    drop_graphs();
+    for (auto& e : pev)
+      if (e) hipEventDestroy(e);
+    for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_fwd, ev_bnd, ev_rev})
+      if (e) hipEventDestroy(e);
     if (st) hipStreamDestroy(st);
+    if (cs) hipStreamDestroy(cs);
   }
 };
 
@@ -386,13 +636,12 @@ template <typename T>
 Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, double kappa,
                const double* wts, const double* qpts, const void* tabs, void* const* ptrs,
                const int64_t* halo_sizes, const int64_t* face_cnt, const int64_t* ghost_cnt,
-               int transport, int nranks, int rank, const void* uid, int64_t group_id,
-               hipStream_t st) {
-  auto* rt = new CGRuntime<T>();
+               int transport, int nranks, int rank, int64_t group_id, hipStream_t st) {
+  auto rt = std::make_unique<CGRuntime<T>>();
   RtConfig& c = rt->cfg;
   std::memcpy(c.latd, latd, sizeof(c.latd));
   std::memcpy(c.own, own, sizeof(c.own));
-  // iparams: version, affine, P, nq, nblocks, nty, ntz, sy, sz, use_graph
+  // iparams: version, affine, P, nq, nblocks, nty, ntz, sy, sz, use_graph, overlap
   c.version = iparams[0];
   c.affine = iparams[1];
   c.P = iparams[2];
@@ -403,16 +652,19 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   c.sy = iparams[7];
   c.sz = iparams[8];
   rt->use_graph = iparams[9] != 0;
+  const bool overlap = iparams[10] != 0;
   c.kappa = kappa;
   c.wts.assign(wts, wts + c.nq);
   c.qpts.assign(qpts, qpts + c.nq);
   rt->apply = apply_fn<T>(c.version, c.P);
-  if (!rt->apply) {
-    delete rt;
-    return nullptr;
+  if (!rt->apply || !tabs) return nullptr;
+  if (c.version == 5) {
+    rt->tabs = static_cast<const T*>(tabs);  // the operator's device table buffer
+  } else {
+    const T* tb = static_cast<const T*>(tabs);
+    rt->tabs_host.assign(tb, tb + kFusedTabMax);
+    rt->tabs = rt->tabs_host.data();
   }
-  const T* tb = static_cast<const T*>(tabs);
-  rt->tabs.assign(tb, tb + 384);  // kFusedTabMax (lap_fused.h)
   int i = 0;
   rt->x = static_cast<T*>(ptrs[i++]);
   rt->r = static_cast<T*>(ptrs[i++]);
@@ -438,11 +690,11 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   rt->nranks = nranks;
   rt->ext = st;
   if (hipStreamCreateWithFlags(&rt->st, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&rt->ev_in, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&rt->ev_out, hipEventDisableTiming) != hipSuccess) {
-    delete rt;
+      hipStreamCreateWithFlags(&rt->cs, hipStreamNonBlocking) != hipSuccess)
     return nullptr;
-  }
+  for (hipEvent_t* e : {&rt->ev_in, &rt->ev_out, &rt->ev_fork, &rt->ev_fwd, &rt->ev_bnd,
+                        &rt->ev_rev})
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
   rt->face_cnt.assign(face_cnt, face_cnt + nranks);
   rt->ghost_cnt.assign(ghost_cnt, ghost_cnt + nranks);
   rt->face_off.assign(nranks, 0);
@@ -452,15 +704,24 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
     rt->ghost_off[p] = rt->ghost_off[p - 1] + rt->ghost_cnt[p - 1];
   }
   rt->halo = nranks > 1 && (rt->face_total + rt->ghost_total) > 0;
-  if (transport == 1 && nranks > 1) {  // RCCL
+  // overlapped schedule: x whole, so only the last tile row (y ghost plane)
+  // and the last tile column (z ghost plane) touch ghosts
+  const BdxLattice L = BdxLattice::from(c.latd);
+  const int g1 = static_cast<int>(L.gh[1]), g2 = static_cast<int>(L.gh[2]);
+  if (overlap && rt->halo && L.gh[0] == 0 && (g1 || g2)) {
+    const int iy = c.nty - g1, iz = c.ntz - g2;  // interior tile extents
+    const int h = (iy + 1) / 2;
+    const int ra[4] = {0, h, 0, iz}, rb[4] = {h, iy, 0, iz};
+    const int r1[4] = {iy, c.nty, 0, c.ntz}, r2[4] = {0, iy, iz, c.ntz};
+    std::memcpy(rt->rect_a, ra, sizeof(ra));
+    std::memcpy(rt->rect_b, rb, sizeof(rb));
+    std::memcpy(rt->rect_r1, r1, sizeof(r1));
+    std::memcpy(rt->rect_r2, r2, sizeof(r2));
+    rt->split = true;
+  }
+  if (transport == 1 && nranks > 1) {  // RCCL: connected by bdx_rt_connect
     auto t = std::make_unique<RcclTransport>();
     t->nranks = nranks;
-    ncclUniqueId id;
-    std::memcpy(&id, uid, sizeof(id));
-    if (ncclCommInitRank(&t->comm, nranks, id, rank) != ncclSuccess) {
-      delete rt;
-      return nullptr;
-    }
     rt->tr = std::move(t);
   } else if (transport == 2 && nranks > 1) {  // in-process threads
     auto t = std::make_unique<ThreadTransport>();
@@ -479,12 +740,18 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
     t->rank = rank;
     rt->tr = std::move(t);
   } else {  // single rank: no communication
-    auto t = std::make_unique<RcclTransport>();
-    t->nranks = 1;
-    rt->tr = std::move(t);
+    rt->tr = std::make_unique<NoTransport>();
     rt->halo = false;
+    rt->split = false;
   }
-  return new Handle{sizeof(T) == 8, rt};
+  return new Handle{sizeof(T) == 8, rt.release()};
+}
+
+template <typename F>
+auto with_rt(void* h, F&& f) {
+  auto* H = static_cast<Handle*>(h);
+  if (H->is_f64) return f(static_cast<CGRuntime<double>*>(H->rt));
+  return f(static_cast<CGRuntime<float>*>(H->rt));
 }
 
 }  // namespace
@@ -507,8 +774,8 @@ int bdx_rt_rccl_selftest(double* buf, int n, hipStream_t st) {
   ncclUniqueId id;
   if (ncclGetUniqueId(&id) != ncclSuccess) return -10;
   RcclTransport t;
-  t.nranks = 1;
-  if (ncclCommInitRank(&t.comm, 1, id, 0) != ncclSuccess) return -11;
+  if (t.connect(id, 1, 0)) return -11;
+  if (t.ranks() != 1) return -19;
   const std::vector<int64_t> cnt{n}, off0{0}, offn{n}, offg{2 * static_cast<int64_t>(n) + 2};
   int rc = t.exchange(buf, cnt, off0, buf, cnt, offn, sizeof(double), st);
   if (!rc) rc = t.allreduce_sum(buf + 2 * n, 2, st);
@@ -529,7 +796,11 @@ int bdx_rt_rccl_selftest(double* buf, int n, hipStream_t st) {
   if (hipStreamEndCapture(cs, &g) != hipSuccess || !g) rc = rc ? rc : -15;
   if (!rc && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) rc = -16;
   if (!rc && hipGraphLaunch(ge, cs) != hipSuccess) rc = -17;
-  if (!rc && hipStreamSynchronize(cs) != hipSuccess) rc = -18;
+  hipEvent_t ev = nullptr;
+  if (!rc && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) rc = -18;
+  if (!rc && hipEventRecord(ev, cs) != hipSuccess) rc = -18;
+  if (!rc) rc = t.wait(ev);  // the watchdog-bounded host wait of the runtime
+  if (ev) hipEventDestroy(ev);
   if (ge) hipGraphExecDestroy(ge);
   if (g) hipGraphDestroy(g);
   hipStreamDestroy(cs);
@@ -540,48 +811,92 @@ void* bdx_rt_create(int is_f64, const int64_t* latd, const int64_t* own, const i
                     double kappa, const double* wts, const double* qpts, const void* tabs,
                     void* const* ptrs, const int64_t* halo_sizes, const int64_t* face_cnt,
                     const int64_t* ghost_cnt, int transport, int nranks, int rank,
-                    const void* uid, int64_t group_id, hipStream_t st) {
+                    int64_t group_id, hipStream_t st) {
   if (is_f64)
     return create<double>(latd, own, iparams, kappa, wts, qpts, tabs, ptrs, halo_sizes,
-                          face_cnt, ghost_cnt, transport, nranks, rank, uid, group_id, st);
+                          face_cnt, ghost_cnt, transport, nranks, rank, group_id, st);
   return create<float>(latd, own, iparams, kappa, wts, qpts, tabs, ptrs, halo_sizes, face_cnt,
-                       ghost_cnt, transport, nranks, rank, uid, group_id, st);
+                       ghost_cnt, transport, nranks, rank, group_id, st);
+}
+
+// Open the runtime's RCCL communicator (collective over the ranks; every
+// rank calls it only after all ranks created their runtime).  Bounded by the
+// watchdog deadline.  0 on success (or when the transport is not RCCL).
+int bdx_rt_connect(void* h, const void* uid, int rank) {
+  return with_rt(h, [&](auto* rt) -> int {
+    auto* t = dynamic_cast<RcclTransport*>(rt->tr.get());
+    if (!t) return 0;
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    return t->connect(id, t->nranks, rank);
+  });
+}
+
+// Ranks of the transport (ncclCommCount for RCCL; -1 if not connected).
+int bdx_rt_comm_count(void* h) {
+  return with_rt(h, [](auto* rt) { return rt->tr->ranks(); });
+}
+
+// 1 if the overlapped (split-tile, two-stream) schedule is active.
+int bdx_rt_overlap(void* h) {
+  return with_rt(h, [](auto* rt) { return rt->split ? 1 : 0; });
 }
 
 // Reset the CG state after a new prologue (p_a zeroed by the caller).
 int bdx_rt_reset(void* h) {
-  auto* H = static_cast<Handle*>(h);
-  if (H->is_f64) {
-    auto* rt = static_cast<CGRuntime<double>*>(H->rt);
+  return with_rt(h, [](auto* rt) {
     rt->it = 0;
     rt->x_lag = false;
-  } else {
-    auto* rt = static_cast<CGRuntime<float>*>(H->rt);
-    rt->it = 0;
-    rt->x_lag = false;
-  }
-  return 0;
+    return 0;
+  });
+}
+
+// Bind a new iterate buffer x (DeviceCG.start with another x): the captured
+// graphs hold the old pointer, so they are dropped and re-captured.
+int bdx_rt_bind_x(void* h, void* x) {
+  return with_rt(h, [&](auto* rt) {
+    using T = std::remove_pointer_t<decltype(rt->x)>;
+    if (rt->x != static_cast<T*>(x)) {
+      const hipError_t e = hipStreamSynchronize(rt->st);
+      rt->drop_graphs();
+      rt->x = static_cast<T*>(x);
+      return static_cast<int>(e);
+    }
+    return 0;
+  });
 }
 
 int bdx_rt_iterate(void* h, long n) {
-  auto* H = static_cast<Handle*>(h);
-  if (H->is_f64) return static_cast<CGRuntime<double>*>(H->rt)->iterate(n);
-  return static_cast<CGRuntime<float>*>(H->rt)->iterate(n);
+  return with_rt(h, [&](auto* rt) { return rt->iterate(n); });
+}
+
+// Host wait for everything iterate() queued, bounded by the RCCL deadline
+// (a hung peer aborts the communicator instead of blocking forever).
+int bdx_rt_wait(void* h) {
+  return with_rt(h, [](auto* rt) { return rt->tr->wait(rt->ev_out); });
+}
+
+// n eager CG iterations with hipEvent phase timers; out (9 doubles, mean ms):
+//   0 forward halo (comm stream: pack, exchange, unpack)
+//   1 operator, interior tiles A (serial schedule: the whole operator)
+//   2 ghost-touching tiles + ghost finalize (waits for the forward halo)
+//   3 reverse halo (pack, exchange; serial: + unpack-add)
+//   4 operator, interior tiles B
+//   5 unpack-add + reduce + all-reduce(p.Ap) (waits for the reverse halo)
+//   6 r update + r.r
+//   7 all-reduce(r.r)
+//   8 whole iteration
+int bdx_rt_profile(void* h, long n, double* out, int nout) {
+  return with_rt(h, [&](auto* rt) { return rt->profile(n, out, nout); });
 }
 
 // it (iterations done) and whether steady-state graphs are in use.
 int bdx_rt_state(void* h, long* it, int* graphs) {
-  auto* H = static_cast<Handle*>(h);
-  if (H->is_f64) {
-    auto* rt = static_cast<CGRuntime<double>*>(H->rt);
+  return with_rt(h, [&](auto* rt) {
     *it = rt->it;
     *graphs = rt->use_graph && (rt->graph_ok[0] || rt->graph_ok[1]);
-  } else {
-    auto* rt = static_cast<CGRuntime<float>*>(H->rt);
-    *it = rt->it;
-    *graphs = rt->use_graph && (rt->graph_ok[0] || rt->graph_ok[1]);
-  }
-  return 0;
+    return 0;
+  });
 }
 
 void bdx_rt_destroy(void* h) {

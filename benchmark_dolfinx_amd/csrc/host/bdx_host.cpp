@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../include/bdx_lattice.h"
+#include "../include/bdx_watchdog.h"
 
 namespace {
 
@@ -563,5 +564,35 @@ int bdx_host_version() { return 1; }
 
 BDX_HOST_API(double, f64)
 BDX_HOST_API(float, f32)
+
+// CPU unit test of the RCCL deadline policy (csrc/include/bdx_watchdog.h, used
+// by the native runtime around every blocking RCCL call and host wait): a
+// busy scope of `busy_s` under a `timeout_s` deadline, with the communicator
+// reporting an asynchronous error from `err_after_s` on (< 0: never).
+// Returns 1 if the watchdog fired (0 if not); *fire_s = seconds from the
+// start of the scope to the abort callback (-1 if it never ran), *reason =
+// 1 deadline / 2 async error.
+int bdx_watchdog_selftest(double timeout_s, double busy_s, double err_after_s, double* fire_s,
+                          int* reason) {
+  const int64_t t0 = bdx::Watchdog::now_ns();
+  std::atomic<int64_t> fired_at{0};
+  bdx::Watchdog w(
+      timeout_s,
+      [&] { return err_after_s >= 0 && (bdx::Watchdog::now_ns() - t0) * 1e-9 >= err_after_s; },
+      [&] { fired_at.store(bdx::Watchdog::now_ns()); });
+  w.start(0.005);
+  {
+    bdx::Watchdog::Busy scope(&w);
+    const int64_t end = t0 + static_cast<int64_t>(busy_s * 1e9);
+    // the "blocked call": returns early once the abort has run, like an
+    // RCCL call unblocked by ncclCommAbort
+    while (bdx::Watchdog::now_ns() < end && !w.fired())
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  w.stop();
+  *fire_s = fired_at.load() ? (fired_at.load() - t0) * 1e-9 : -1.0;
+  *reason = w.reason();
+  return w.fired() ? 1 : 0;
+}
 
 }  // extern "C"

@@ -98,6 +98,7 @@ def _run_loop(op, pb, x, u, nreps, use_cg, dev_cg):
     if use_cg:
         if pb.platform == "gpu":
             dev_cg.solve(op, x, u, nreps)
+            dev_cg.wait()  # bounded by the RCCL deadline (native runtime)
         else:
             cg_solve(op, pb, x, u, nreps, 0.0)
     else:

@@ -57,12 +57,25 @@ def compute_mesh_size(ndofs_global: int, degree: int) -> tuple[int, int, int]:
     return nx
 
 
-def partition_grid(nranks: int, ncells: tuple[int, int, int]) -> tuple[int, int, int]:
+def partition_grid(nranks: int, ncells: tuple[int, int, int],
+                   whole_x: bool = False) -> tuple[int, int, int]:
     """Factor nranks into (px, py, pz) minimising the cut area.
 
     Cut area = sum_d (p_d - 1) * (cross-section normal to d).  Ties prefer
     splitting x first (x-planes are contiguous in the z-fastest layout).
+
+    ``whole_x``: never split x (px = 1) when a (y, z) split exists.  The fused
+    GPU kernels march along x over (y, z) tiles; with x whole only the last
+    tile row / column touches a ghost plane, so the native runtime runs every
+    other tile while the halo exchange is in flight (csrc/hip/runtime.hip).
+    That costs some cut area (8 ranks on a cube: 1x2x4, +32 %) for halos that
+    are hidden instead of exposed.
     """
+    if whole_x:
+        try:
+            return partition_grid(nranks, (1, ncells[1], ncells[2]))
+        except ValueError:
+            pass
     nx, ny, nz = ncells
     best = None
     for px in range(1, nranks + 1):
@@ -261,8 +274,8 @@ class LocalLattice:
 
 
 def make_local_lattice(rank: int, nranks: int, ncells: tuple[int, int, int],
-                       degree: int) -> LocalLattice:
-    pgrid = partition_grid(nranks, ncells)
+                       degree: int, whole_x: bool = False) -> LocalLattice:
+    pgrid = partition_grid(nranks, ncells, whole_x)
     px, py, pz = pgrid
     rz = rank % pz
     ry = (rank // pz) % py

@@ -139,7 +139,13 @@ class FusedLaplacianGPU:
                 raise RuntimeError(f"no fused tables for nd={t.nd} nq={t.nq}")
             host = np.zeros(ntab, dtype=np.float64 if pb.dtype == torch.float64 else np.float32)
             ftab(t.nd, t.nq, ptr(t.phi0), ptr(second), ptr(host))
-        self.tabs = host  # host memory: copied into the kernel arguments
+        if version == 5:
+            # fused5 reads its tables through a pointer: a device buffer owned
+            # by this operator (a captured graph keeps reading its own tables)
+            self.tabs_host = host
+            self.tabs = torch.from_numpy(host).to(dev)
+        else:
+            self.tabs = host  # host memory: copied into the kernel arguments
         if version >= 2:
             self._apply2 = getattr(self.lib, f"bdx_fused{version}_apply_{pb.suf}_p{P}")
         else:
@@ -170,7 +176,7 @@ class FusedLaplacianGPU:
                                 ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(x), ptr(y),
                                 ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(pb.xv),
                                 ptr(pb.kc), ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials),
-                                beta_num, beta_den, xa_num, xa_den, self.nty, self.ntz,
+                                beta_num, beta_den, xa_num, xa_den, self.nty, self.ntz, None,
                                 _stream()), "fused2_apply")
         else:
             _check(self._apply(self.geom_code, mode, ptr(pb.latd), t.nq, ptr(t.phi0),
@@ -205,17 +211,20 @@ class FusedLaplacianGPU:
         self._own = np.array(self.pb.lat.owned_hi, dtype=np.int64)
         if self.runtime == "native":
             if self._rt is None or self._rt.cg is not cg:
-                from ..solvers.native import NativeCGRuntime
+                from ..solvers.native import NativeCGRuntime, NativeRuntimeUnavailable
                 if self._rt is not None:
                     self._rt.close()
                 try:
                     self._rt = NativeCGRuntime(self, cg)
-                except RuntimeError as e:  # e.g. RCCL bootstrap failure: stay correct
+                except NativeRuntimeUnavailable as e:
+                    # raised on every rank alike (construction is collective),
+                    # so all ranks take the Python driver of the same kernels
                     import sys
                     print(f"[bdx] native CG runtime unavailable ({e}); using the Python "
                           f"driver of the same kernels", file=sys.stderr)
                     self.runtime, self._rt = "python", None
             if self._rt is not None:
+                self._rt.bind_x(x)  # DeviceCG.start may pass another iterate
                 self._rt.reset()
 
     def cg_iterate(self, cg, n):

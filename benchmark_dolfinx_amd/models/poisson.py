@@ -17,6 +17,7 @@ MatFreeLaplacianGPU/CPU (src/laplacian.hpp:87-771) and MatrixOperator
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -73,7 +74,8 @@ def cells_all_parallelepipeds(X: np.ndarray) -> bool:
 class PoissonProblem:
     def __init__(self, comm: Comm, ncells, degree: int, qmode: int = 1,
                  use_gauss: bool = False, dtype=torch.float64, platform: str = "gpu",
-                 perturb: float = 0.0, coefficient: str = "constant", shear: float = 0.0):
+                 perturb: float = 0.0, coefficient: str = "constant", shear: float = 0.0,
+                 partition: str | None = None):
         if use_gauss and qmode == 0:
             # same validation as the reference (src/laplacian.hpp:197-198, Q5)
             raise RuntimeError("Expecting identity matrix for qmode=0")
@@ -87,7 +89,15 @@ class PoissonProblem:
         self.qmode = qmode
         self.use_gauss = use_gauss
         self.tables = OperatorTables(degree, qmode, use_gauss)
-        self.lat: LocalLattice = make_local_lattice(comm.rank, comm.size, tuple(ncells), degree)
+        # "yz": keep the march axis x whole (halo/compute overlap of the fused
+        # GPU runtime); "xyz": minimum cut area.  Default: yz on the GPU.
+        partition = partition or os.environ.get("BDX_PARTITION") or (
+            "yz" if platform == "gpu" else "xyz")
+        if partition not in ("yz", "xyz"):
+            raise ValueError(f"unknown partition policy {partition!r}")
+        self.partition = partition
+        self.lat: LocalLattice = make_local_lattice(comm.rank, comm.size, tuple(ncells), degree,
+                                                    whole_x=partition == "yz")
         npdt = _np_dtype(dtype)
         with timed("~setup mesh"):
             xv = vertex_coordinates(self.lat, perturb, shear=shear).astype(npdt)

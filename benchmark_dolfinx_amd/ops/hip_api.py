@@ -41,7 +41,7 @@ def declare(lib) -> None:
             name = f"bdx_fused{v}_apply_{suf}_p{P}"
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
-                               vp, vp, f64, vp, vp, i32, i32, i32, i32, i32, i32, vp])
+                               vp, vp, f64, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp])
         _d(lib, f"bdx_fused_finalize_{suf}", [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp])
         _d(lib, f"bdx_cg_update_iface_{suf}", [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32,
                                                 vp, i32, i32, i32, vp, vp])
@@ -61,7 +61,13 @@ def declare(lib) -> None:
     _d(lib, "bdx_rt_nccl_unique_id", [vp])
     _d(lib, "bdx_rt_rccl_selftest", [vp, i32, vp])
     _d(lib, "bdx_rt_create", [i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
-                              vp, i64, vp], vp)
+                              i64, vp], vp)
+    _d(lib, "bdx_rt_connect", [vp, vp, i32])
+    _d(lib, "bdx_rt_comm_count", [vp])
+    _d(lib, "bdx_rt_overlap", [vp])
+    _d(lib, "bdx_rt_bind_x", [vp, vp])
+    _d(lib, "bdx_rt_wait", [vp])
+    _d(lib, "bdx_rt_profile", [vp, ctypes.c_long, vp, i32])
     _d(lib, "bdx_rt_reset", [vp])
     _d(lib, "bdx_rt_iterate", [vp, ctypes.c_long])
     _d(lib, "bdx_rt_state", [vp, vp, vp])

@@ -118,3 +118,13 @@ def device_info(dev: int = 0) -> str:
     if rc != 0:
         return f"(device info unavailable: hipError {rc})\n"
     return buf.value.decode()
+
+
+def device_name(dev: int = 0) -> str:
+    """hipDeviceProp name + gcnArchName (torch's get_device_name() returns a
+    generic marketing string on this stack)."""
+    info = device_info(dev)
+    fields = dict(line.strip().split(": ", 1) for line in info.splitlines() if ": " in line)
+    name = fields.get("Device", "unknown")
+    arch = fields.get("gcnArch", "")
+    return f"{name} ({arch})" if arch else name

@@ -97,6 +97,32 @@ def hip():
     return _hip
 
 
+def build_flags() -> dict:
+    """Build facts of the loaded HIP library that decide whether a timing is
+    valid: the arch, the library file, and every timing-only phase-drop
+    macro compiled into it (BDX_UPD_DROP, BDX_F4_DROP, BDX_F5_DROP; nonzero
+    values skip work and give wrong numerics -- bench.py refuses them)."""
+    lib = hip()
+    drops = {}
+    for name, key in (("bdx_drop_flags_common", "BDX_UPD_DROP"),
+                      ("bdx_drop_flags_f4", "BDX_F4_DROP")):
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = ctypes.c_int
+            drops[key] = int(fn())
+    f5 = 0
+    for suf in ("f64", "f32"):
+        for P in range(1, 8):
+            name = f"bdx_drop_flags_f5_{suf}_p{P}"
+            if hasattr(lib, name):
+                fn = getattr(lib, name)
+                fn.restype = ctypes.c_int
+                f5 |= int(fn())
+    drops["BDX_F5_DROP"] = f5
+    return {"arch": _build.HIP_ARCH, "hiplib": os.path.basename(_loaded.get("hip", "")),
+            "drops": drops, "valid": not any(drops.values())}
+
+
 def loaded_libraries() -> list[str]:
     out = []
     if _host is not None:

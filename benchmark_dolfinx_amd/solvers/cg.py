@@ -99,6 +99,16 @@ class DeviceCG:
             k.p_update(p, r, scal, nxt, cur)
             self.it += 1
 
+    def wait(self) -> None:
+        """Host wait for the queued iterations.  With the native runtime the
+        wait is bounded by the RCCL deadline (a hung peer raises instead of
+        blocking torch.cuda.synchronize forever)."""
+        rt = getattr(self.op, "_rt", None)
+        if rt is not None:
+            rt.wait()
+        elif self.pb.platform == "gpu":
+            torch.cuda.synchronize()
+
     def solve(self, op, x: torch.Tensor, b: torch.Tensor, max_iter: int) -> int:
         self.start(op, x, b)
         self.iterate(max_iter)

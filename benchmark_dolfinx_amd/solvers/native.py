@@ -5,10 +5,11 @@ the whole iteration loop -- halo exchange, fused operator, reductions,
 all-reduces, r/x updates -- runs in C++ on the current HIP stream, with the
 steady-state iterations replayed from hipGraphs.  Transport:
 
-* ``rccl``   one process per GPU (torchrun); the runtime opens its own RCCL
-  communicator, bootstrapped by exchanging an ncclUniqueId over the existing
-  torch.distributed group, and exchanges halos with grouped ncclSend/ncclRecv
-  to the neighbours only;
+* ``rccl``   one process per GPU (torchrun or bench.py's own launcher); the
+  runtime opens its own RCCL communicator, bootstrapped by exchanging an
+  ncclUniqueId over the existing torch.distributed group, and exchanges halos
+  with grouped ncclSend/ncclRecv to the neighbours only, on a second stream
+  overlapped with the interior tiles of the operator;
 * ``thread`` ranks are threads of one process on one GPU (ThreadComm tests);
 * single rank: no communication.
 """
@@ -26,38 +27,67 @@ from ..ops.kernels import _check, _stream
 from ..ops.native import ptr
 
 
+PHASES = ("halo_fwd", "op_interior_a", "op_boundary", "halo_rev", "op_interior_b",
+          "reduce_allreduce_pap", "update_rr", "allreduce_rr", "iteration")
+
+
+def _agree(comm, ok: bool) -> bool:
+    """True iff every rank reports ok (a MIN all-reduce over the torch group)."""
+    if comm.size == 1:
+        return ok
+    return comm.allreduce_scalar(1.0 if ok else 0.0, "min") > 0.5
+
+
 class NativeCGRuntime:
-    def __init__(self, op, cg, use_graph: bool | None = None):
+    """Handle of one rank's native CG loop.
+
+    Construction is collective and all-or-nothing: every rank first builds
+    its runtime locally (no communication), the ranks agree that all
+    succeeded, then the RCCL communicator is opened (bounded by the
+    watchdog deadline) and the ranks agree again.  If any rank fails at
+    either step every rank releases its handle and raises
+    NativeRuntimeUnavailable, so all ranks take the same fallback (a rank
+    on native RCCL calls and a rank on torch collectives would never match).
+    """
+
+    # test hook: rank whose local creation is made to fail
+    _inject_fail_rank: int | None = None
+
+    def __init__(self, op, cg, use_graph: bool | None = None, overlap: bool | None = None):
         pb = op.pb
         self.op, self.cg, self.pb = op, cg, pb
         self.lib = native.hip()
+        self.h = None
         comm = pb.comm
         halo = pb.halo
         if use_graph is None:
-            # BDX_GRAPH=0 off, 1 (default) single-rank only, 2 also with RCCL
-            # (multi-rank capture of the RCCL calls is supported but has only
-            # been exercised on the driver's multi-GPU node; the replay buys
-            # < 1 % at these kernel times, so it is opt-in there)
+            # BDX_GRAPH=0 off, 1 (default) single rank only, 2 also with RCCL
+            # (the two-stream fork/join iteration captures RCCL calls; that
+            # has not run on a multi-GPU node yet, and the host runs far
+            # ahead of a 6 ms iteration anyway, so it is opt-in there)
             mode = os.environ.get("BDX_GRAPH", "1")
             use_graph = mode == "2" or (mode == "1" and comm.size == 1)
+        if overlap is None:
+            overlap = os.environ.get("BDX_OVERLAP", "1") != "0"
         t = op.t
         self._latd = np.ascontiguousarray(pb.latd, dtype=np.int64)
         self._own = np.array(pb.lat.owned_hi, dtype=np.int64)
         self._ip = np.array([op.version, op.affine_code, pb.degree, t.nq, op.nblocks, op.nty,
-                             op.ntz, op.sy, op.sz, int(use_graph)], dtype=np.int32)
+                             op.ntz, op.sy, op.sz, int(use_graph), int(overlap)],
+                            dtype=np.int32)
         self._wts = np.ascontiguousarray(t.wts, dtype=np.float64)
         self._qpts = np.ascontiguousarray(t.qpts, dtype=np.float64)
         self.upart = torch.zeros(self.lib.bdx_hip_partials_size(), dtype=torch.float64,
                                  device=pb.device)
         fo, gh = halo.owned_faces, halo.ghosts
+        self.x = cg.x
         bufs = [cg.x, cg.r, op.p_old, op.p_new, cg.y, op.yb, op.zb, op.cb, pb.xv, cg.scal,
                 op.partials, self.upart, halo.buf_a, halo.buf_b, fo.table, gh.table, pb.kc]
-        self._keep = bufs
+        self._keep = bufs + [op.tabs]
         self._ptrs = (ctypes.c_void_p * len(bufs))(*[ptr(b) for b in bufs])
         self._hs = np.array([len(fo.boxes), fo.total, len(gh.boxes), gh.total], dtype=np.int64)
         self._fc = np.array(fo.counts, dtype=np.int64)
         self._gc = np.array(gh.counts, dtype=np.int64)
-        uid = (ctypes.c_char * 128)()
         self.group = 0
         if comm.size == 1:
             transport = 0
@@ -66,43 +96,93 @@ class NativeCGRuntime:
             self.group = id(comm.g)
         elif comm.backend == "nccl":
             transport = 1
-            if comm.rank == 0:
-                n = self.lib.bdx_rt_nccl_unique_id(uid)
-                if n <= 0:
-                    raise RuntimeError("ncclGetUniqueId failed")
-            ids = comm.gather_objects(bytes(uid) if comm.rank == 0 else None)
-            ctypes.memmove(uid, ids[0], 128)
         else:
-            raise RuntimeError(f"native CG runtime: no transport for backend {comm.backend!r}")
-        self.transport = ("none", "rccl", "thread")[transport]
-        self.h = self.lib.bdx_rt_create(
-            int(pb.dtype == torch.float64), ptr(self._latd), ptr(self._own), ptr(self._ip),
-            float(pb.kappa), ptr(self._wts), ptr(self._qpts), ptr(op.tabs), self._ptrs,
-            ptr(self._hs), ptr(self._fc), ptr(self._gc), transport, comm.size, comm.rank, uid,
-            self.group, _stream())
-        if not self.h:
-            raise RuntimeError("bdx_rt_create failed (unsupported kernel or RCCL init error)")
+            transport = -1
+        self.transport = {0: "none", 1: "rccl", 2: "thread"}.get(transport, "unsupported")
+        # 1) local creation (no communication)
+        ok = transport >= 0 and comm.rank != self._inject_fail_rank
+        if ok:
+            self.h = self.lib.bdx_rt_create(
+                int(pb.dtype == torch.float64), ptr(self._latd), ptr(self._own), ptr(self._ip),
+                float(pb.kappa), ptr(self._wts), ptr(self._qpts), ptr(op.tabs), self._ptrs,
+                ptr(self._hs), ptr(self._fc), ptr(self._gc), transport, comm.size, comm.rank,
+                self.group, _stream())
+            ok = bool(self.h)
+        if not _agree(comm, ok):
+            self.close()
+            raise NativeRuntimeUnavailable(
+                "bdx_rt_create failed on at least one rank (unsupported kernel, no transport "
+                f"for backend {comm.backend!r}, or an injected failure)")
+        # 2) open the runtime's own RCCL communicator (ncclUniqueId from rank 0
+        #    over the torch group); bounded by the watchdog deadline
+        if transport == 1:
+            uid = (ctypes.c_char * 128)()
+            good = True
+            if comm.rank == 0:
+                good = self.lib.bdx_rt_nccl_unique_id(uid) > 0
+            ids = comm.gather_objects(bytes(uid) if (comm.rank == 0 and good) else None)
+            if ids[0] is None:
+                self.close()
+                raise NativeRuntimeUnavailable("ncclGetUniqueId failed on rank 0")
+            ctypes.memmove(uid, ids[0], 128)
+            ok = self.lib.bdx_rt_connect(self.h, uid, comm.rank) == 0
+            if not _agree(comm, ok):
+                self.close()
+                raise NativeRuntimeUnavailable("ncclCommInitRank failed on at least one rank")
+        self.overlap = bool(self.lib.bdx_rt_overlap(self.h))
+        self.graphs = False
+
+    def comm_ranks(self) -> int:
+        """Ranks of the runtime's own communicator (ncclCommCount for RCCL)."""
+        return int(self.lib.bdx_rt_comm_count(self.h))
+
+    def bind_x(self, x: torch.Tensor) -> None:
+        """Point the runtime at a new iterate (drops the captured graphs)."""
+        if x.data_ptr() != self.x.data_ptr():
+            _check(self.lib.bdx_rt_bind_x(self.h, ptr(x)), "rt_bind_x")
+            self.x = x
+            self._keep[0] = x
 
     def reset(self) -> None:
         _check(self.lib.bdx_rt_reset(self.h), "rt_reset")
 
-    def iterate(self, n: int) -> None:
-        _check(self.lib.bdx_rt_iterate(self.h, int(n)), "rt_iterate")
+    def _sync_state(self) -> None:
         it, graphs = ctypes.c_long(0), ctypes.c_int(0)
         self.lib.bdx_rt_state(self.h, ctypes.byref(it), ctypes.byref(graphs))
         self.cg.it = it.value
         self.graphs = bool(graphs.value)
+
+    def iterate(self, n: int) -> None:
+        _check(self.lib.bdx_rt_iterate(self.h, int(n)), "rt_iterate")
+        self._sync_state()
+
+    def wait(self) -> None:
+        """Host wait for the queued iterations, bounded by the RCCL deadline
+        (BDX_RCCL_TIMEOUT_S): a hung peer raises instead of blocking forever."""
+        _check(self.lib.bdx_rt_wait(self.h), "rt_wait")
+
+    def profile(self, n: int) -> dict:
+        """n eager iterations with hipEvent phase timers -> mean ms per phase."""
+        out = (ctypes.c_double * len(PHASES))()
+        _check(self.lib.bdx_rt_profile(self.h, int(n), out, len(PHASES)), "rt_profile")
+        self._sync_state()
+        return {k: float(v) for k, v in zip(PHASES, out)}
 
     def close(self) -> None:
         if getattr(self, "h", None):
             torch.cuda.synchronize()
             self.lib.bdx_rt_destroy(self.h)
             self.h = None
-            if self.group:
-                self.lib.bdx_rt_release_group(self.group)
+        if getattr(self, "group", 0):
+            self.lib.bdx_rt_release_group(self.group)
+            self.group = 0
 
     def __del__(self):
         try:
             self.close()
         except Exception:  # pragma: no cover - interpreter shutdown
             pass
+
+
+class NativeRuntimeUnavailable(RuntimeError):
+    """Raised on every rank when the native runtime cannot run on all ranks."""

@@ -1,0 +1,177 @@
+"""GPU tests of the native CG runtime (csrc/hip/runtime.hip): the overlapped
+two-stream schedule (halo exchange hidden under interior tiles) against one
+rank, the all-or-nothing construction across ranks, per-operator device
+tables under graph replay, re-binding the iterate, hipEvent phase timers,
+and bench.py's own entry point on one GPU."""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from benchmark_dolfinx_amd.models.fused import FusedLaplacianGPU, fused_supported
+from benchmark_dolfinx_amd.models.poisson import MatFreeLaplacianCPU, PoissonProblem
+from benchmark_dolfinx_amd.parallel.comm import Comm, run_threaded
+from benchmark_dolfinx_amd.solvers.cg import DeviceCG, cg_solve
+from benchmark_dolfinx_amd.solvers.native import NativeCGRuntime
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _job(comm, nc, P, nreps, version, partition, pert=0.0, dtype=torch.float64,
+         coefficient="constant"):
+    pb = PoissonProblem(comm, nc, P, 1, False, dtype, "gpu", pert, coefficient,
+                        partition=partition)
+    if not fused_supported(pb, version):
+        return None
+    u = pb.assemble_rhs()
+    x = pb.new_vector()
+    op = FusedLaplacianGPU(pb, "otf", version, affine=version in (4, 5) or pert == 0.0)
+    cg = DeviceCG(pb)
+    cg.solve(op, x, u, nreps)
+    cg.wait()
+    rt = op._rt
+    info = (rt.overlap, rt.transport, rt.comm_ranks(), op.runtime) if rt else (
+        False, "python", None, op.runtime)
+    xn = pb.norm(x)
+    op.close()
+    return xn, pb.lat.pgrid, info
+
+
+# meshes large enough that interior (ghost-free) tiles exist on every rank
+@pytest.mark.parametrize("version,P,nc", [(2, 3, (5, 22, 26)), (3, 3, (5, 22, 26)),
+                                          (4, 3, (5, 22, 26)), (5, 6, (3, 9, 10)),
+                                          (5, 4, (4, 14, 13))])
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_overlap_schedule_matches_one_rank(ranks, version, P, nc):
+    ref = run_threaded(1, _job, nc, P, 12, version, "yz")[0]
+    if ref is None:
+        pytest.skip(f"fused{version} does not cover P={P}")
+    got = run_threaded(ranks, _job, nc, P, 12, version, "yz")
+    for xn, pgrid, (overlap, transport, nr, runtime) in got:
+        assert pgrid[0] == 1 and runtime == "native" and transport == "thread" and nr == ranks
+        assert overlap, "x whole and a halo: the split schedule must be active"
+        assert abs(xn - ref[0]) <= 1e-11 * abs(ref[0]), (xn, ref[0])
+    # the serial schedule (x split by the min-cut partition) gives the same iterate
+    ser = run_threaded(ranks, _job, nc, P, 12, version, "xyz")
+    for xn, pgrid, (overlap, *_rest) in ser:
+        assert overlap == (pgrid[0] == 1)
+        assert abs(xn - ref[0]) <= 1e-11 * abs(ref[0])
+
+
+def test_overlap_schedule_random_kappa_fp32():
+    nc = (4, 18, 20)
+    ref = run_threaded(1, _job, nc, 3, 10, 3, "yz", 0.0, torch.float32, "random")[0]
+    got = run_threaded(4, _job, nc, 3, 10, 3, "yz", 0.0, torch.float32, "random")
+    for xn, _, (overlap, *_rest) in got:
+        assert overlap
+        assert abs(xn - ref[0]) <= 2e-5 * abs(ref[0])
+
+
+def test_create_failure_on_one_rank_falls_back_on_every_rank():
+    nc = (4, 10, 12)
+    ref = run_threaded(1, _job, nc, 3, 8, 2, "yz")[0]
+    NativeCGRuntime._inject_fail_rank = 1
+    try:
+        got = run_threaded(3, _job, nc, 3, 8, 2, "yz")
+    finally:
+        NativeCGRuntime._inject_fail_rank = None
+    for xn, _, (_ov, transport, _nr, runtime) in got:
+        assert runtime == "python" and transport == "python"  # all ranks, not only rank 1
+        assert abs(xn - ref[0]) <= 1e-11 * abs(ref[0])
+
+
+def _host_cg(nc, P, qm, g, n):
+    cpu = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "cpu")
+    xc = cpu.new_vector()
+    cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), n)
+    return cpu, xc
+
+
+def test_fused5_operators_keep_their_own_tables_under_graph_replay():
+    """Two fused5 operators of the same (P, T) with different tables (qmode 1
+    vs qmode 0 GLL; Gauss) interleave their graph-replayed iterations; each
+    must match its own host CG (a shared device table would mix them)."""
+    nc, P = (3, 4, 5), 5
+    cases = [(1, False), (0, False), (1, True)]
+    runs = []
+    for qm, g in cases:
+        pb = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "gpu")
+        if not fused_supported(pb, 5):
+            pytest.skip("no fused5 instance")
+        op = FusedLaplacianGPU(pb, "otf", 5)
+        cg = DeviceCG(pb)
+        x = pb.new_vector()
+        cg.start(op, x, pb.assemble_rhs())
+        runs.append((pb, op, cg, x))
+    for _ in range(6):  # interleave: 6 rounds x 4 iterations each, graphs replayed
+        for pb, op, cg, x in runs:
+            cg.iterate(4)
+    torch.cuda.synchronize()
+    for (qm, g), (pb, op, cg, x) in zip(cases, runs):
+        assert op._rt is not None and op._rt.graphs
+        cpu, xc = _host_cg(nc, P, qm, g, 24)
+        rel = (cpu.owned(x.cpu()) - cpu.owned(xc)).abs().max().item() / xc.abs().max().item()
+        assert rel < 1e-10, (qm, g, rel)
+        op.close()
+
+
+def test_devicecg_solves_twice_with_different_iterates():
+    nc = (5, 6, 7)
+    pb = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu")
+    u = pb.assemble_rhs()
+    op = FusedLaplacianGPU(pb, "otf", 4 if fused_supported(pb, 4) else 3)
+    cg = DeviceCG(pb)
+    x1, x2 = pb.new_vector(), pb.new_vector()
+    cg.solve(op, x1, u, 20)
+    cg.solve(op, x2, u, 11)
+    torch.cuda.synchronize()
+    cpu, r20 = _host_cg(nc, 3, 1, False, 20)
+    _, r11 = _host_cg(nc, 3, 1, False, 11)
+    for x, ref in ((x1, r20), (x2, r11)):
+        rel = (cpu.owned(x.cpu()) - cpu.owned(ref)).abs().max().item() / ref.abs().max().item()
+        assert rel < 1e-10, rel
+    op.close()
+
+
+def test_phase_profile_single_and_threaded():
+    def job(comm):
+        pb = PoissonProblem(comm, (4, 16, 18), 3, 1, False, torch.float64, "gpu")
+        op = FusedLaplacianGPU(pb, "otf", 3)
+        cg = DeviceCG(pb)
+        x = pb.new_vector()
+        cg.solve(op, x, pb.assemble_rhs(), 4)
+        ph = op._rt.profile(3)
+        it = cg.it
+        op.close()
+        return ph, it
+    for ranks in (1, 2):
+        for ph, it in run_threaded(ranks, job):
+            assert it == 7
+            assert ph["iteration"] > 0 and ph["op_interior_a"] > 0
+            assert all(v >= 0 for v in ph.values())
+            if ranks > 1:
+                assert ph["halo_fwd"] > 0 and ph["halo_rev"] > 0
+
+
+def test_bench_entry_point_one_gpu():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--dofs-per-gpu", "2000000",
+                        "--steps", "5", "--warmup", "2"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["steps"] == 5
+    cfg = line["config"]
+    assert cfg["build_flags"]["valid"] and cfg["comm"]["transport"] == "none"
+    assert cfg["comm"]["rccl_ranks"] == 1
+    assert cfg["phases_ms"]["iteration"] > 0
+    assert "gfx950" in cfg["device"]
+    assert np.isfinite(cfg["y_norm"]) and cfg["y_norm"] > 0
