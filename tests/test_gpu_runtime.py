@@ -41,7 +41,7 @@ def _job(comm, nc, P, nreps, version, partition, pert=0.0, dtype=torch.float64,
         False, "python", None, op.runtime)
     xn = pb.norm(x)
     op.close()
-    return xn, pb.lat.pgrid, info
+    return xn, pb.lat.pgrid, info + (tuple(pb.lat.gh),)
 
 
 # meshes large enough that interior (ghost-free) tiles exist on every rank
@@ -54,14 +54,16 @@ def test_overlap_schedule_matches_one_rank(ranks, version, P, nc):
     if ref is None:
         pytest.skip(f"fused{version} does not cover P={P}")
     got = run_threaded(ranks, _job, nc, P, 12, version, "yz")
-    for xn, pgrid, (overlap, transport, nr, runtime) in got:
+    for xn, pgrid, (overlap, transport, nr, runtime, gh) in got:
         assert pgrid[0] == 1 and runtime == "native" and transport == "thread" and nr == ranks
-        assert overlap, "x whole and a halo: the split schedule must be active"
+        # x whole: every rank with an upper (y or z) neighbour splits its tiles
+        assert overlap == bool(gh[1] or gh[2]), (overlap, gh)
         assert abs(xn - ref[0]) <= 1e-11 * abs(ref[0]), (xn, ref[0])
+    assert any(r[2][0] for r in got)
     # the serial schedule (x split by the min-cut partition) gives the same iterate
     ser = run_threaded(ranks, _job, nc, P, 12, version, "xyz")
-    for xn, pgrid, (overlap, *_rest) in ser:
-        assert overlap == (pgrid[0] == 1)
+    for xn, pgrid, (overlap, *_rest, gh) in ser:
+        assert overlap == (pgrid[0] == 1 and bool(gh[1] or gh[2]))
         assert abs(xn - ref[0]) <= 1e-11 * abs(ref[0])
 
 
@@ -69,8 +71,8 @@ def test_overlap_schedule_random_kappa_fp32():
     nc = (4, 18, 20)
     ref = run_threaded(1, _job, nc, 3, 10, 3, "yz", 0.0, torch.float32, "random")[0]
     got = run_threaded(4, _job, nc, 3, 10, 3, "yz", 0.0, torch.float32, "random")
-    for xn, _, (overlap, *_rest) in got:
-        assert overlap
+    assert any(r[2][0] for r in got)
+    for xn, _, _info in got:
         assert abs(xn - ref[0]) <= 2e-5 * abs(ref[0])
 
 
@@ -82,7 +84,7 @@ def test_create_failure_on_one_rank_falls_back_on_every_rank():
         got = run_threaded(3, _job, nc, 3, 8, 2, "yz")
     finally:
         NativeCGRuntime._inject_fail_rank = None
-    for xn, _, (_ov, transport, _nr, runtime) in got:
+    for xn, _, (_ov, transport, _nr, runtime, _gh) in got:
         assert runtime == "python" and transport == "python"  # all ranks, not only rank 1
         assert abs(xn - ref[0]) <= 1e-11 * abs(ref[0])
 
