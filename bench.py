@@ -58,6 +58,9 @@ def parse_args(argv=None):
     ap.add_argument("--perturb", type=float, default=0.0,
                     help="--geom_perturb_fact of the reference: random x-perturbation of "
                          "the vertices (general trilinear cells)")
+    ap.add_argument("--mesh", default=None,
+                    help="experiments only: explicit global cell counts NX,NY,NZ instead of "
+                         "the config's DoF target")
     ap.add_argument("--profile-steps", type=int, default=5,
                     help="extra eager iterations with hipEvent phase timers (0: none)")
     return ap.parse_args(argv)
@@ -88,7 +91,8 @@ def run(comm, a) -> dict | None:
                              f"drops {flags['drops']} (wrong numerics); refusing to time it "
                              f"(BDX_ALLOW_DROP=1 runs it, marked invalid)")
     dtype = torch.float64 if bits == 64 else torch.float32
-    nx = compute_mesh_size(dpg * n, degree)
+    nx = (tuple(int(v) for v in a.mesh.split(",")) if a.mesh
+          else compute_mesh_size(dpg * n, degree))
 
     def log(msg):
         if comm.rank == 0:
