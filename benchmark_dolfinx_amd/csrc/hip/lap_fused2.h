@@ -72,7 +72,9 @@ struct Fused2Args {
   int bcx_lo, bcx_hi;            // local index of the global boundary plane, -1 if none
   int bcy_lo, bcy_hi, bcz_lo, bcz_hi;
   int nty, ntz;
-  int ty0, tz0, rwz, nblk;       // tile rectangle of this launch: [ty0, ty0 + nblk / rwz) x [tz0, tz0 + rwz)
+  int ty0, tz0, rwz, rtiles;     // tile rectangle of this launch: [ty0, ty0 + rtiles / rwz) x [tz0, tz0 + rwz)
+  int nseg, seglen;              // x segments per tile (work item = (tile, segment)), cells per segment
+  int nblk;                      // workgroups of the launch = rtiles * nseg
   int beta_num, beta_den;        // CG: beta = scal[num] / scal[den]; num < 0 -> 0
   int xa_num, xa_den;            // CG: alpha_prev = scal[num] / scal[den]; num < 0 -> no x update
   T kappa;
@@ -749,7 +751,10 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
   a.ntz = ntz;
   a.ty0 = a.tz0 = 0;
   a.rwz = ntz;
-  a.nblk = nty * ntz;
+  a.rtiles = nty * ntz;
+  a.nseg = 1;
+  a.seglen = a.ncx;
+  a.nblk = a.rtiles;
   return 0;
 }
 
@@ -767,7 +772,51 @@ inline int fused_set_rect(Fused2Args<T>& a, const int* rect) {
   a.ty0 = ty0;
   a.tz0 = tz0;
   a.rwz = tz1 > tz0 ? tz1 - tz0 : 1;
-  a.nblk = (ty1 - ty0) * (tz1 - tz0);
+  a.rtiles = (ty1 - ty0) * (tz1 - tz0);
+  a.nblk = a.rtiles * a.nseg;
+  return 0;
+}
+
+// x segmentation.  A launch of R tiles on a chip that holds W workgroups at
+// once runs ceil(R / W) rounds of whole x-marches; at the benchmark sizes the
+// last round is nearly empty (1 GPU, Q3: 3136 tiles = 6.1 rounds of 512 ->
+// 7 rounds, measured 12 % slower per DoF than an exact 6 or 7).  Cutting each
+// tile's march into S segments makes R * S shorter work items whose rounds
+// pack evenly.  A segment [a, b) of cell layers starts one layer early (a - 1,
+// "redundant": computed but never written) so the partial sum it carries into
+// plane a*P completes that plane locally; it writes planes [a*P, b*P) (plus
+// the last plane if b is the end) and stages layers a .. b-1 (the redundant
+// layer's planes belong to the previous segment).  No inter-workgroup
+// synchronisation, bitwise identical to S = 1 except for the order of the
+// p.Ap partial sums (one per work item).
+//   mode argument of the apply entry points: kind | (S << 8), S = 0 -> 1.
+inline int fused_choose_segments(int tiles, int ncx, int resident) {
+  if (tiles <= 0 || ncx <= 1 || resident <= 0) return 1;
+  int best = 1;
+  double best_cost = 1e300;
+  for (int S = 1; S <= 16 && S <= ncx; ++S) {
+    const int len = (ncx + S - 1) / S;
+    const int segs = (ncx + len - 1) / len;
+    const double rounds = static_cast<double>((static_cast<int64_t>(tiles) * segs + resident - 1) /
+                                              resident);
+    // per work item: its layers, the redundant layer, and ~1 layer of
+    // unpipelined prologue
+    const double cost = rounds * (len + (S > 1 ? 2.0 : 1.0));
+    if (cost < best_cost * 0.995) {
+      best_cost = cost;
+      best = segs;
+    }
+  }
+  return best;
+}
+
+template <typename T>
+inline int fused_set_segments(Fused2Args<T>& a, int nseg) {
+  if (nseg < 1) nseg = 1;
+  if (nseg > a.ncx) nseg = a.ncx > 0 ? a.ncx : 1;
+  a.seglen = (a.ncx + nseg - 1) / nseg;
+  a.nseg = a.seglen > 0 ? (a.ncx + a.seglen - 1) / a.seglen : 1;
+  a.nblk = a.rtiles * a.nseg;
   return 0;
 }
 
@@ -782,6 +831,7 @@ inline int fused_set_rect(Fused2Args<T>& a, const int* rect) {
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
+    mode &= 0xff; /* whole-x marches: the segment count is ignored */   \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \

@@ -129,10 +129,17 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   const int nblk = gridDim.x, ob = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
-  const int ty = A.ty0 + bid / A.rwz, tz = A.tz0 + bid % A.rwz;
+  // work item = (tile of the launch rectangle, x segment); see fused_set_segments
+  const int tix = bid % A.rtiles, seg = bid / A.rtiles;
+  const int ty = A.ty0 + tix / A.rwz, tz = A.tz0 + tix % A.rwz;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
   const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
   const int ncx = A.ncx;
+  // own cell layers [sa, cend); the march starts one layer early (redundant)
+  // in every segment but the first
+  const int sa = seg * A.seglen;
+  const int cend = (sa + A.seglen < ncx) ? sa + A.seglen : ncx;
+  const int cbeg = sa > 0 ? sa - 1 : 0;
   const bool top_y = (ty == A.nty - 1), top_z = (tz == A.ntz - 1);
   const int ey = (y0 + DY <= Ly) ? DY : Ly - y0;
   const int ez = (z0 + DZ <= Lz) ? DZ : Lz - z0;
@@ -169,9 +176,12 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     if (gy < A.owny && gz < A.ownz) f |= kRownYZ;
     return f;
   };
+  // stage one input node of the prologue layer; wr = false (a redundant
+  // layer: the previous segment owns these planes) computes the value only
   auto stage = [&](int f, int gx, const T* __restrict__ ul, T* __restrict__ pn, T* __restrict__ yl,
-                   int goff) -> T {
+                   int goff, bool wr) -> T {
     T v;
+    if (!wr) f &= ~kOwnT;
     if constexpr (MODE == kFusedCG) {
       const T po = A.pold[(ul - A.u) + goff];
       v = ul[goff] + beta * po;
@@ -276,13 +286,19 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     }
   }
 
-  // ---- prologue: layer 0 (planes 0..P), vertex planes 0/1, zero carry
-  for (int e = tid; e < ND * PL; e += NT) {
-    const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
-    const int f = yz_flags(ly, lz);
-    T v = T(0);
-    if (f & kValid) v = stage(f, pl, A.u, A.pnew, A.y, (pl * Ly + y0 + ly) * ld + z0 + lz);
-    s_u[0][pl * PLP + ly * DZP + lz] = v;
+  // ---- prologue: layer cbeg (planes 0..P), vertex planes cbeg/cbeg+1, zero carry
+  {
+    const int64_t l0 = static_cast<int64_t>(cbeg) * P * A.ps;
+    const bool wr = cbeg == sa;  // not a redundant layer
+    for (int e = tid; e < ND * PL; e += NT) {
+      const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      const int f = yz_flags(ly, lz);
+      T v = T(0);
+      if (f & kValid)
+        v = stage(f, cbeg * P + pl, A.u + l0, A.pnew + l0, A.y + l0,
+                  (pl * Ly + y0 + ly) * ld + z0 + lz, wr);
+      s_u[0][pl * PLP + ly * DZP + lz] = v;
+    }
   }
   for (int e = tid; e < 2 * NV; e += NT) {
     const int k = e % NV;
@@ -293,7 +309,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       const int gy = ty * TY + vy, gz = tz * TZ + vz;
       if (gy <= A.n1 && gz <= A.n2) off = (gy * (A.n2 + 1) + gz) * 3 + d;
     }
-    s_X[0][e] = off >= 0 ? A.xv[(e / NV) * A.vps + off] : T(0);
+    s_X[0][e] = off >= 0 ? A.xv[static_cast<int64_t>(cbeg + e / NV) * A.vps + off] : T(0);
   }
   for (int e = tid; e < PL; e += NT) s_c[0][e] = T(0);
 
@@ -301,15 +317,17 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
 
   const int64_t kc_ps = static_cast<int64_t>(A.n1) * A.n2;
   const int64_t kc_cell = static_cast<int64_t>(ty * TY + cy) * A.n2 + tz * TZ + cz;
-  if (A.kc) s_kc[0][c] = cell_on ? A.kc[kc_cell] : T(0);  // read after the loop-top barrier
+  if (A.kc) s_kc[0][c] = cell_on ? A.kc[cbeg * kc_ps + kc_cell] : T(0);  // read after the loop-top barrier
   // Everything loaded so far (the per-lane x matrices Xr, the prologue
   // layer) has landed before the march starts: without this explicit wait the
   // waitcnt pass carries the Xr loads as pending around the loop and makes
   // their uses inside the MFMA core wait for each layer's prefetch batch.
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  for (int cx = 0; cx < ncx; ++cx) {
-    const int cur = cx & 1, nxt = cur ^ 1;
-    const bool last = (cx == ncx - 1);
+  for (int cx = cbeg; cx < cend; ++cx) {
+    const int cur = (cx - cbeg) & 1, nxt = cur ^ 1;
+    const bool last = (cx == cend - 1);   // end of this segment
+    const bool glast = (cx == ncx - 1);   // end of the march
+    const bool red = (cx < sa);           // redundant layer: carry only
     __syncthreads();
 
     // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
@@ -451,7 +469,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     const bdx_f64x4 ye = acc0 + acc1;
     // lane holds y_e[cell][x = xi][y = r][z = g], r = 0..3
     if constexpr (MODE == kFusedCG) {
-      if (cell_on) {
+      if (cell_on && !red) {
 #pragma unroll
         for (int r = 0; r < ND; ++r)
           pap += static_cast<double>(ub[xi * PLP + r * DZP]) * static_cast<double>(ye[r]);
@@ -530,6 +548,9 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
           s_c[nxt][rem] = v;
           continue;
         }
+        // a redundant layer only carries; a segment's end plane is completed
+        // (and written) by the next segment
+        if (red || (pl == P && !glast)) continue;
         const int gxx = cx * P + pl;
         const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
         const int kind = (m >> 4) & 3;
@@ -565,7 +586,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
-    if (tid == 0) A.partials[ty * A.ntz + tz] = t;  // tile-indexed: launch-split invariant
+    // indexed by (tile, segment): invariant under any launch split
+    if (tid == 0) A.partials[(ty * A.ntz + tz) * A.nseg + seg] = t;
   }
 }
 

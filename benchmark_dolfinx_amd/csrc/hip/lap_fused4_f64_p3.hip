@@ -15,6 +15,8 @@ extern "C" int bdx_fused4_apply_f64_p3(
   Fused2Args<double> a;
   BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));
   BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));
+  BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));
+  mode &= 0xff;
   a.u = u;
   a.pold = pold;
   a.pnew = pnew;
@@ -52,3 +54,16 @@ extern "C" int bdx_fused4_tile(int* ty, int* tz) {
 
 // Timing-only phase drops compiled into this TU (0 in a valid build).
 extern "C" int bdx_drop_flags_f4() { return BDX_F4_DROP; }
+
+// x segments per tile for a launch of `tiles` tiles marching `ncx` layers
+// (fused_choose_segments with this kernel's resident workgroups).
+extern "C" int bdx_fused4_segments(int tiles, int ncx) {
+  constexpr int TY = BDX_F4_TY, TZ = BDX_F4_TZ;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lap_fused4_kernel<TY, TZ, kFusedCG>,
+                                                   TY * TZ * 16, 0) != hipSuccess)
+    return 1;
+  return fused_choose_segments(tiles, ncx, per_cu * cus);
+}

@@ -648,6 +648,7 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
+    mode &= 0xff; /* whole-x marches: the segment count is ignored */   \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \

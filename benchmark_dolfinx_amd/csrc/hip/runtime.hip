@@ -358,7 +358,7 @@ enum Mark {
 struct RtConfig {
   int64_t latd[17];
   int64_t own[3];
-  int version, affine, P, nq, nblocks, nty, ntz, sy, sz;
+  int version, affine, P, nq, nblocks, nty, ntz, sy, sz, nseg;
   double kappa;
   std::vector<double> wts, qpts;
 };
@@ -444,7 +444,7 @@ struct CGRuntime {
     T* pold = (k % 2 == 0) ? pa : pb;
     T* pnew = (k % 2 == 0) ? pb : pa;
     auto op = [&](const int* rect, hipStream_t s) {
-      return apply(1, cfg.affine, cfg.latd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
+      return apply(1 | (cfg.nseg << 8), cfg.affine, cfg.latd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
                    pnew, x, y, yb, zb, cb, xv, kc, tabs, cfg.kappa, scal, partials,
                    first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1,
                    cfg.nty, cfg.ntz, rect, s);
@@ -641,7 +641,8 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   RtConfig& c = rt->cfg;
   std::memcpy(c.latd, latd, sizeof(c.latd));
   std::memcpy(c.own, own, sizeof(c.own));
-  // iparams: version, affine, P, nq, nblocks, nty, ntz, sy, sz, use_graph, overlap
+  // iparams: version, affine, P, nq, nblocks, nty, ntz, sy, sz, use_graph, overlap, nseg
+  // (nblocks = nty * ntz * nseg p.Ap partials)
   c.version = iparams[0];
   c.affine = iparams[1];
   c.P = iparams[2];
@@ -653,6 +654,7 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   c.sz = iparams[8];
   rt->use_graph = iparams[9] != 0;
   const bool overlap = iparams[10] != 0;
+  c.nseg = iparams[11] > 0 ? iparams[11] : 1;
   c.kappa = kappa;
   c.wts.assign(wts, wts + c.nq);
   c.qpts.assign(qpts, qpts + c.nq);

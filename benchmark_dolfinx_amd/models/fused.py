@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -98,7 +99,20 @@ class FusedLaplacianGPU:
         self.yb = torch.zeros(max(1, Lx * (self.nty - 1) * Lz), dtype=dt, device=dev)
         self.zb = torch.zeros(max(1, Lx * Ly * (self.ntz - 1)), dtype=dt, device=dev)
         self.cb = torch.zeros(max(1, Lx * (self.nty - 1) * (self.ntz - 1)), dtype=dt, device=dev)
-        self.nblocks = self.nty * self.ntz
+        # x segments per tile (work items = tiles x segments, see
+        # fused_set_segments in lap_fused2.h): sized against the chip's
+        # resident workgroups so the last round of the launch is not nearly
+        # empty.  BDX_SEGMENTS=<n> forces n (1 = whole-x marches).
+        self.nseg = 1
+        seg_fn = {4: "bdx_fused4_segments"}.get(version)
+        if seg_fn and hasattr(self.lib, seg_fn):
+            forced = os.environ.get("BDX_SEGMENTS", "")
+            self.nseg = int(forced) if forced else int(getattr(self.lib, seg_fn)(
+                self.nty * self.ntz, lat.n[0]))
+            self.nseg = max(1, min(self.nseg, max(1, lat.n[0])))
+            seglen = -(-lat.n[0] // self.nseg)
+            self.nseg = -(-lat.n[0] // seglen)  # no empty segments (as the kernel)
+        self.nblocks = self.nty * self.ntz * self.nseg
         self.partials = torch.zeros(self.nblocks, dtype=torch.float64, device=dev)
         self.G = None
         if geometry == "stored":
@@ -172,7 +186,8 @@ class FusedLaplacianGPU:
                 xa_num=-1, xa_den=-1, finalize=True):
         pb, t = self.pb, self.t
         if self.version >= 2:
-            _check(self._apply2(mode, self.affine_code, ptr(pb.latd), t.nq, ptr(t.wts),
+            _check(self._apply2(mode | (self.nseg << 8), self.affine_code, ptr(pb.latd), t.nq,
+                                ptr(t.wts),
                                 ptr(t.qpts), ptr(u), ptr(pold), ptr(pnew), ptr(x), ptr(y),
                                 ptr(self.yb), ptr(self.zb), ptr(self.cb), ptr(pb.xv),
                                 ptr(pb.kc), ptr(self.tabs), pb.kappa, ptr(scal), ptr(self.partials),

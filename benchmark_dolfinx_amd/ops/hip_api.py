@@ -57,6 +57,9 @@ def declare(lib) -> None:
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
     if hasattr(lib, "bdx_fused4_tile"):
         _d(lib, "bdx_fused4_tile", [vp, vp])
+    for name in ("bdx_fused4_segments",):
+        if hasattr(lib, name):
+            _d(lib, name, [i32, i32])
     # native CG runtime (runtime.hip)
     _d(lib, "bdx_rt_nccl_unique_id", [vp])
     _d(lib, "bdx_rt_rccl_selftest", [vp, i32, vp])

@@ -73,7 +73,7 @@ class NativeCGRuntime:
         self._latd = np.ascontiguousarray(pb.latd, dtype=np.int64)
         self._own = np.array(pb.lat.owned_hi, dtype=np.int64)
         self._ip = np.array([op.version, op.affine_code, pb.degree, t.nq, op.nblocks, op.nty,
-                             op.ntz, op.sy, op.sz, int(use_graph), int(overlap)],
+                             op.ntz, op.sy, op.sz, int(use_graph), int(overlap), op.nseg],
                             dtype=np.int32)
         self._wts = np.ascontiguousarray(t.wts, dtype=np.float64)
         self._qpts = np.ascontiguousarray(t.qpts, dtype=np.float64)
