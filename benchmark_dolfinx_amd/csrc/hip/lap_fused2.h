@@ -121,7 +121,14 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   const int nblk = gridDim.x, ob = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
-  const int ty = A.ty0 + bid / A.rwz, tz = A.tz0 + bid % A.rwz;
+  // work item = (tile of the launch rectangle, x segment); see fused_set_segments
+  const int tix = bid % A.rtiles, seg = bid / A.rtiles;
+  const int ty = A.ty0 + tix / A.rwz, tz = A.tz0 + tix % A.rwz;
+  // own cell layers [sa, cend); the march starts one layer early (redundant)
+  // in every segment but the first
+  const int sa = seg * A.seglen;
+  const int cend = (sa + A.seglen < A.ncx) ? sa + A.seglen : A.ncx;
+  const int cbeg = sa > 0 ? sa - 1 : 0;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
   const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
   const int ncx = A.ncx;
@@ -161,9 +168,12 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     return f;
   };
   // Input value of a staged dof + its CG / Dirichlet side effects.
+  // (wr = false: a redundant layer, whose planes the previous segment owns:
+  // the value only, no side effects)
   auto stage = [&](int f, int gx, const T* __restrict__ ul, T* __restrict__ pn, T* __restrict__ yl,
-                   int goff) -> T {
+                   int goff, bool wr) -> T {
     T v;
+    if (!wr) f &= ~kOwnT;
     if constexpr (MODE == kFusedCG) {
       const T po = A.pold[(ul - A.u) + goff];
       v = ul[goff] + beta * po;
@@ -270,13 +280,19 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     }
   }
 
-  // ---- prologue: layer 0 (planes 0..P), vertex planes 0/1, zero carry
-  for (int e = tid; e < ND * PL; e += NT) {
-    const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
-    const int f = yz_flags(ly, lz);
-    T v = T(0);
-    if (f & kValid) v = stage(f, pl, A.u, A.pnew, A.y, (pl * Ly + y0 + ly) * ld + z0 + lz);
-    s_u[0][pl * PLP + ly * DZP + lz] = v;
+  // ---- prologue: layer cbeg (planes 0..P), vertex planes cbeg/cbeg+1, zero carry
+  {
+    const int64_t l0 = static_cast<int64_t>(cbeg) * P * A.ps;
+    const bool wr = cbeg == sa;  // not a redundant layer
+    for (int e = tid; e < ND * PL; e += NT) {
+      const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      const int f = yz_flags(ly, lz);
+      T v = T(0);
+      if (f & kValid)
+        v = stage(f, cbeg * P + pl, A.u + l0, A.pnew + l0, A.y + l0,
+                  (pl * Ly + y0 + ly) * ld + z0 + lz, wr);
+      s_u[0][pl * PLP + ly * DZP + lz] = v;
+    }
   }
   for (int e = tid; e < 2 * NV; e += NT) {
     const int k = e % NV;
@@ -287,7 +303,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
       const int gy = ty * TY + vy, gz = tz * TZ + vz;
       if (gy <= A.n1 && gz <= A.n2) off = (gy * (A.n2 + 1) + gz) * 3 + d;
     }
-    s_X[0][e] = off >= 0 ? A.xv[(e / NV) * A.vps + off] : T(0);
+    s_X[0][e] = off >= 0 ? A.xv[static_cast<int64_t>(cbeg + e / NV) * A.vps + off] : T(0);
   }
   for (int e = tid; e < PL; e += NT) s_c[0][e] = T(0);
 
@@ -295,9 +311,11 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};
   T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};
 
-  for (int cx = 0; cx < ncx; ++cx) {
-    const int cur = cx & 1, nxt = cur ^ 1;
-    const bool last = (cx == ncx - 1);
+  for (int cx = cbeg; cx < cend; ++cx) {
+    const int cur = (cx - cbeg) & 1, nxt = cur ^ 1;
+    const bool last = (cx == cend - 1);   // end of this segment
+    const bool glast = (cx == ncx - 1);   // end of the march
+    const bool red = (cx < sa);           // redundant layer: carry only
     __syncthreads();
 
     // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
@@ -593,7 +611,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
     // ------------------------------------------------ element vectors -> LDS
     const bool dof_lane = cell_on && a < ND && b < ND;
     if constexpr (MODE == kFusedCG) {
-      if (dof_lane) {
+      if (dof_lane && !red) {
 #pragma unroll
         for (int i = 0; i < ND; ++i)
           pap += static_cast<double>(ua[i * PLP + b]) * static_cast<double>(ye[i]);
@@ -628,6 +646,9 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
           s_c[nxt][rem] = v;
           continue;
         }
+        // a redundant layer only carries; a segment's end plane is completed
+        // (and written) by the next segment
+        if (red || (pl == P && !glast)) continue;
         const int gxx = cx * P + pl;
         const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
         const int kind = (m >> 4) & 3;
@@ -696,7 +717,8 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
-    if (tid == 0) A.partials[ty * A.ntz + tz] = t;  // tile-indexed: launch-split invariant
+    // indexed by (tile, segment): invariant under any launch split
+    if (tid == 0) A.partials[(ty * A.ntz + tz) * A.nseg + seg] = t;
   }
 }
 
@@ -714,6 +736,23 @@ int launch_fused2(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, 
   else
     lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 0><<<nblk, S::threads, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());
+}
+
+// Workgroups of a fused2 CG instance the chip holds at once (segment sizing).
+template <typename T, int ND, int NQ>
+int fused2_resident(int affine) {
+  using TF = TileFor<NQ>;
+  using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const hipError_t e =
+      affine ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                   &per_cu, lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 1>, S::threads, 0)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                   &per_cu, lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 0>, S::threads, 0);
+  return e == hipSuccess ? per_cu * cus : 0;
 }
 
 template <typename T>
@@ -831,7 +870,8 @@ inline int fused_set_segments(Fused2Args<T>& a, int nseg) {
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
-    mode &= 0xff; /* whole-x marches: the segment count is ignored */   \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
+    mode &= 0xff;                                                                  \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \
@@ -863,4 +903,9 @@ inline int fused_set_segments(Fused2Args<T>& a, int nseg) {
       return mode == kFusedCG ? launch_fused2<T, PP + 1, PP + 2, kFusedCG>(affine_ok, a, tb, st) \
                               : launch_fused2<T, PP + 1, PP + 2, kFusedAction>(affine_ok, a, tb, st); \
     return static_cast<int>(hipErrorInvalidValue);                                 \
+  }                                                                                \
+  extern "C" int bdx_fused2_segments_##SUF##_p##PP(int affine_ok, int nq, int tiles, int ncx) { \
+    const int res = nq == PP + 1 ? fused2_resident<T, PP + 1, PP + 1>(affine_ok)   \
+                                 : fused2_resident<T, PP + 1, PP + 2>(affine_ok);  \
+    return fused_choose_segments(tiles, ncx, res);                                 \
   }

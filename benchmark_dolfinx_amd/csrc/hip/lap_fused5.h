@@ -125,10 +125,17 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
   const int nblk = gridDim.x, ob = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
-  const int ty = A.ty0 + bid / A.rwz, tz = A.tz0 + bid % A.rwz;
+  // work item = (tile of the launch rectangle, x segment); see fused_set_segments
+  const int tix = bid % A.rtiles, seg = bid / A.rtiles;
+  const int ty = A.ty0 + tix / A.rwz, tz = A.tz0 + tix % A.rwz;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
   const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
   const int ncx = A.ncx;
+  // own cell layers [sa, cend); the march starts one layer early (redundant)
+  // in every segment but the first
+  const int sa = seg * A.seglen;
+  const int cend = (sa + A.seglen < ncx) ? sa + A.seglen : ncx;
+  const int cbeg = sa > 0 ? sa - 1 : 0;
   const bool top_y = (ty == A.nty - 1), top_z = (tz == A.ntz - 1);
   const int ey = (y0 + DY <= Ly) ? DY : Ly - y0;
   const int ez = (z0 + DZ <= Lz) ? DZ : Lz - z0;
@@ -164,9 +171,12 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     if (gy < A.owny && gz < A.ownz) f |= kRownYZ;
     return f;
   };
+  // stage one input node of the prologue layer; wr = false (a redundant
+  // layer: the previous segment owns these planes) computes the value only
   auto stage = [&](int f, int gx, const T* __restrict__ ul, T* __restrict__ pn, T* __restrict__ yl,
-                   int goff) -> T {
+                   int goff, bool wr) -> T {
     T v;
+    if (!wr) f &= ~kOwnT;
     if constexpr (MODE == kFusedCG) {
       const T po = A.pold[(ul - A.u) + goff];
       v = ul[goff] + beta * po;
@@ -273,13 +283,19 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     }
   }
 
-  // ---- prologue: layer 0 (planes 0..P), vertex planes 0/1, zero carry
-  for (int e = tid; e < ND * PL; e += NT) {
-    const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
-    const int f = yz_flags(ly, lz);
-    T v = T(0);
-    if (f & kValid) v = stage(f, pl, A.u, A.pnew, A.y, (pl * Ly + y0 + ly) * ld + z0 + lz);
-    s_u[0][pl * PLP + ly * DZP + lz] = v;
+  // ---- prologue: layer cbeg (planes 0..P), vertex planes cbeg/cbeg+1, zero carry
+  {
+    const int64_t l0 = static_cast<int64_t>(cbeg) * P * A.ps;
+    const bool wr = cbeg == sa;  // not a redundant layer
+    for (int e = tid; e < ND * PL; e += NT) {
+      const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
+      const int f = yz_flags(ly, lz);
+      T v = T(0);
+      if (f & kValid)
+        v = stage(f, cbeg * P + pl, A.u + l0, A.pnew + l0, A.y + l0,
+                  (pl * Ly + y0 + ly) * ld + z0 + lz, wr);
+      s_u[0][pl * PLP + ly * DZP + lz] = v;
+    }
   }
   for (int e = tid; e < 2 * NV; e += NT) {
     const int k = e % NV;
@@ -290,7 +306,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
       const int gy = ty * TY + vy, gz = tz * TZ + vz;
       if (gy <= A.n1 && gz <= A.n2) off = (gy * (A.n2 + 1) + gz) * 3 + d;
     }
-    s_X[0][e] = off >= 0 ? A.xv[(e / NV) * A.vps + off] : T(0);
+    s_X[0][e] = off >= 0 ? A.xv[static_cast<int64_t>(cbeg + e / NV) * A.vps + off] : T(0);
   }
   for (int e = tid; e < PL; e += NT) s_c[0][e] = T(0);
 
@@ -328,10 +344,12 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
 
   const int64_t kc_ps = static_cast<int64_t>(A.n1) * A.n2;
   const int64_t kc_cell = static_cast<int64_t>(ty * TY + cy) * A.n2 + tz * TZ + cz;
-  T kc_cur = (A.kc && cell_on) ? A.kc[kc_cell] : A.kappa;
-  for (int cx = 0; cx < ncx; ++cx) {
-    const int cur = cx & 1, nxt = cur ^ 1;
-    const bool last = (cx == ncx - 1);
+  T kc_cur = (A.kc && cell_on) ? A.kc[cbeg * kc_ps + kc_cell] : A.kappa;
+  for (int cx = cbeg; cx < cend; ++cx) {
+    const int cur = (cx - cbeg) & 1, nxt = cur ^ 1;
+    const bool last = (cx == cend - 1);   // end of this segment
+    const bool glast = (cx == ncx - 1);   // end of the march
+    const bool red = (cx < sa);           // redundant layer: carry only
     __syncthreads();
 
     // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
@@ -493,7 +511,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     }
     // element dot p_e . (A_e p_e): lane holds y_e[i = la][j][k = lb]
     if constexpr (MODE == kFusedCG) {
-      if (cell_on) {
+      if (cell_on && !red) {
 #pragma unroll
         for (int j = 0; j < ND; ++j)
           pap += static_cast<double>(ucell[la * PLP + j * DZP + lb]) * static_cast<double>(ye[j]);
@@ -524,6 +542,9 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
           s_c[nxt][rem] = v;
           continue;
         }
+        // a redundant layer only carries; a segment's end plane is completed
+        // (and written) by the next segment
+        if (red || (pl == P && !glast)) continue;
         const int gxx = cx * P + pl;
         const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
         const int kind = (m >> 4) & 3;
@@ -593,7 +614,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
-    if (tid == 0) A.partials[ty * A.ntz + tz] = t;  // tile-indexed: launch-split invariant
+    // indexed by (tile, segment): invariant under any launch split
+    if (tid == 0) A.partials[(ty * A.ntz + tz) * A.nseg + seg] = t;
   }
 }
 
@@ -648,7 +670,8 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
-    mode &= 0xff; /* whole-x marches: the segment count is ignored */   \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
+    mode &= 0xff;                                                                  \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \
@@ -676,6 +699,21 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     return pack_tables5<T>(nd, nq, phi0, Dd, wts, out);                            \
   }                                                                                \
   extern "C" int bdx_drop_flags_f5_##SUF##_p##PP() { return BDX_F5_DROP; }          \
+  extern "C" int bdx_fused5_segments_##SUF##_p##PP(int affine_ok, int tiles, int ncx) { \
+    int per_cu = 0, dev = 0, cus = 0;                                              \
+    hipError_t e = hipGetDevice(&dev);                                             \
+    if (e == hipSuccess)                                                           \
+      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev); \
+    if (e == hipSuccess)                                                           \
+      e = affine_ok == 2                                                           \
+              ? hipOccupancyMaxActiveBlocksPerMultiprocessor(                      \
+                    &per_cu, lap_fused5_kernel<T, PP + 1, 2, kFusedCG>,            \
+                    F5Shape<T, PP + 1, 2>::NT, 0)                                  \
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(                      \
+                    &per_cu, lap_fused5_kernel<T, PP + 1, 4, kFusedCG>,            \
+                    F5Shape<T, PP + 1, 4>::NT, 0);                                 \
+    return e == hipSuccess ? fused_choose_segments(tiles, ncx, per_cu * cus) : 1;  \
+  }                                                                                \
   extern "C" int bdx_fused5_tile_p##PP##_##SUF(int affine_ok, int* ty, int* tz) {  \
     *ty = affine_ok == 2 ? F5Tile<PP + 1, 2>::TY : F5Tile<PP + 1, 4>::TY;          \
     *tz = affine_ok == 2 ? F5Tile<PP + 1, 2>::TZ : F5Tile<PP + 1, 4>::TZ;          \

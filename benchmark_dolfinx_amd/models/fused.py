@@ -104,11 +104,18 @@ class FusedLaplacianGPU:
         # resident workgroups so the last round of the launch is not nearly
         # empty.  BDX_SEGMENTS=<n> forces n (1 = whole-x marches).
         self.nseg = 1
-        seg_fn = {4: "bdx_fused4_segments"}.get(version)
+        seg_fn = {2: f"bdx_fused2_segments_{pb.suf}_p{pb.degree}",
+                  3: f"bdx_fused3_segments_{pb.suf}_p{pb.degree}",
+                  4: "bdx_fused4_segments",
+                  5: f"bdx_fused5_segments_{pb.suf}_p{pb.degree}"}.get(version)
         if seg_fn and hasattr(self.lib, seg_fn):
             forced = os.environ.get("BDX_SEGMENTS", "")
-            self.nseg = int(forced) if forced else int(getattr(self.lib, seg_fn)(
-                self.nty * self.ntz, lat.n[0]))
+            args = (self.nty * self.ntz, lat.n[0])
+            if version == 5:
+                args = (self.affine_code,) + args
+            elif version in (2, 3):
+                args = (self.affine_code, t.nq) + args
+            self.nseg = int(forced) if forced else int(getattr(self.lib, seg_fn)(*args))
             self.nseg = max(1, min(self.nseg, max(1, lat.n[0])))
             seglen = -(-lat.n[0] // self.nseg)
             self.nseg = -(-lat.n[0] // seglen)  # no empty segments (as the kernel)

@@ -37,6 +37,9 @@ def declare(lib) -> None:
             if hasattr(lib, name):
                 _d(lib, name, [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                vp, vp, vp, vp, f64, vp, vp, i32, i32, i32, i32, vp])
+        for P, v in [(P, v) for P in range(1, 8) for v in (2, 3)]:
+            if hasattr(lib, f"bdx_fused{v}_segments_{suf}_p{P}"):
+                _d(lib, f"bdx_fused{v}_segments_{suf}_p{P}", [i32, i32, i32, i32])
         for P, v in [(P, v) for P in range(1, 8) for v in (2, 3, 4, 5)]:
             name = f"bdx_fused{v}_apply_{suf}_p{P}"
             if hasattr(lib, name):
@@ -54,6 +57,7 @@ def declare(lib) -> None:
             if hasattr(lib, f"bdx_fused5_tables_{suf}_p{P}"):
                 _d(lib, f"bdx_fused5_tables_{suf}_p{P}", [i32, i32, vp, vp, vp, vp])
                 _d(lib, f"bdx_fused5_tile_p{P}_{suf}", [i32, vp, vp])
+                _d(lib, f"bdx_fused5_segments_{suf}_p{P}", [i32, i32, i32])
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
     if hasattr(lib, "bdx_fused4_tile"):
         _d(lib, "bdx_fused4_tile", [vp, vp])

@@ -310,44 +310,53 @@ def test_fused5_partition_invariance(ranks, shear, P, nc):
 
 
 # ---------------------------------------------------------------- x segments
+SEG_CASES = [  # version, P, perturb, dtype
+    (4, 3, 0.0, torch.float64), (5, 6, 0.0, torch.float64), (5, 4, 0.0, torch.float32),
+    (2, 3, 0.2, torch.float64), (3, 3, 0.2, torch.float64), (3, 5, 0.0, torch.float32),
+    (2, 2, 0.1, torch.float64)]
+
+
 @pytest.mark.parametrize("nseg", ["1", "2", "3", "5", "13", ""])
 @pytest.mark.parametrize("kappa", ["constant", "random"])
-def test_fused4_x_segments_cg_and_action(monkeypatch, nseg, kappa):
-    """fused4 with the x-march cut into segments (each starting with a
-    redundant, unwritten layer) matches the CPU operator (action) and host CG
-    for any segment count, incl. the automatic choice ("")."""
+@pytest.mark.parametrize("version,P,pert,dt", SEG_CASES)
+def test_fused_x_segments_cg_and_action(monkeypatch, version, P, pert, dt, nseg, kappa):
+    """The fused kernels with the x-march cut into segments (each starting
+    with a redundant, unwritten layer) match the CPU operator (action) and
+    host CG for any segment count, incl. the automatic choice ("")."""
     monkeypatch.setenv("BDX_SEGMENTS", nseg)
-    nc = (13, 6, 9)
-    gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", 0.0, kappa)
-    _skip_unsupported(gpu, 4)
-    cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", 0.0, kappa)
-    op = FusedLaplacianGPU(gpu, "otf", 4)
+    nc = (13, 5, 6) if P >= 5 else (13, 6, 9)
+    gpu = PoissonProblem(Comm(), nc, P, 1, False, dt, "gpu", pert, kappa)
+    _skip_unsupported(gpu, version)
+    cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", pert, kappa)
+    op = FusedLaplacianGPU(gpu, "otf", version, affine=pert == 0.0)
     if nseg:
-        assert op.nseg == min(int(nseg), -(-13 // -(-13 // int(nseg))))
+        n = int(nseg)
+        assert op.nseg == -(-13 // -(-13 // n)), (op.nseg, n)
     rng = np.random.default_rng(5)
     u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
     yc = cpu.new_vector()
     MatFreeLaplacianCPU(cpu).apply(u64, yc)
-    yg = torch.full(gpu.lat.shape, float("nan"), dtype=torch.float64, device=gpu.device)
-    op.apply(u64.to(gpu.device), yg)
+    yg = torch.full(gpu.lat.shape, float("nan"), dtype=dt, device=gpu.device)
+    op.apply(u64.to(gpu.device, dt), yg)
     o = cpu.owned
-    err = (o(yg.cpu()) - o(yc)).abs().max().item()
-    assert err <= 1e-12 * 50 * max(1.0, yc.abs().max().item()), err
+    err = (o(yg.double().cpu()) - o(yc)).abs().max().item()
+    assert err <= _tol(dt) * 50 * max(1.0, yc.abs().max().item()), err
     xg = gpu.new_vector()
     DeviceCG(gpu).solve(op, xg, gpu.assemble_rhs(), 25)
     xc = cpu.new_vector()
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 25)
-    rel = (o(xg.cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
-    assert rel < 1e-10, rel
+    rel = (o(xg.double().cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
+    assert rel < (1e-10 if dt == torch.float64 else 2e-4), rel
     op.close()
 
 
 @pytest.mark.parametrize("nseg", ["2", "4"])
 @pytest.mark.parametrize("ranks", [2, 4])
-def test_fused4_x_segments_partition_invariance(monkeypatch, nseg, ranks):
+@pytest.mark.parametrize("version,pert", [(4, 0.0), (5, 0.0), (3, 0.1)])
+def test_fused_x_segments_partition_invariance(monkeypatch, version, pert, nseg, ranks):
     monkeypatch.setenv("BDX_SEGMENTS", nseg)
-    ref = run_threaded(1, _cg_job, (11, 14, 17), 3, 12, "otf", 4, 0.0, "native")[0]
-    got = run_threaded(ranks, _cg_job, (11, 14, 17), 3, 12, "otf", 4, 0.0, "native")
+    ref = run_threaded(1, _cg_job, (11, 14, 17), 3, 12, "otf", version, pert, "native")[0]
+    got = run_threaded(ranks, _cg_job, (11, 14, 17), 3, 12, "otf", version, pert, "native")
     for r in got:
         for a, b in zip(r, ref):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
