@@ -24,6 +24,8 @@
 // update, Dirichlet identity rows, p.Ap partials) and the atomic-free gather
 // with tile-interface buffers -- is fused3's (lap_fused3.h).
 #pragma once
+#include <cstdlib>
+
 #include "lap_fused2.h"
 
 #ifndef BDX_F4_TY
@@ -74,7 +76,7 @@ __device__ __forceinline__ double f4_mat(const double* tab, int id, int r, int c
   return id == 3 ? tab[32 + c * 4 + r] : tab[id * 16 + r * 4 + c];
 }
 
-template <int TY, int TZ, int MODE>
+template <int TY, int TZ, int MODE, int DEPTH>
 __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     lap_fused4_kernel(Fused2Args<double> A, FusedTables<double> tb) {
   using T = double;
@@ -323,43 +325,62 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   // waitcnt pass carries the Xr loads as pending around the loop and makes
   // their uses inside the MFMA core wait for each layer's prefetch batch.
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  for (int cx = cbeg; cx < cend; ++cx) {
+  // Prefetch of layer cx + DEPTH (its planes 1..P, vertex plane cx + DEPTH + 1
+  // and cell coefficient) into one register set.  Every load is issued
+  // unconditionally (past the segment it re-reads layer 0, unused), so each
+  // layer issues the same number of loads and the wait for a set can be a
+  // counted vmcnt that leaves the younger set in flight.
+  struct PF {
+    T r[NPF], p[NPF], x[NPF];
+    T v[NPV];
+    T kc;
+  };
+  constexpr int NLD = (MODE == kFusedCG ? 3 : 1) * NPF + NPV + 1;  // loads per set
+  const T* __restrict__ kcp = A.kc ? A.kc : A.xv;
+  auto issue = [&](PF& f, int cl) __attribute__((always_inline)) {
+    const bool in = cl < cend;
+    const int64_t lpf = in ? static_cast<int64_t>(cl) * P * A.ps : 0;
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      f.r[k] = T(0);
+      f.p[k] = T(0);
+      f.x[k] = T(0);
+      if constexpr ((BDX_F4_DROP & 4) == 0) {
+        f.r[k] = A.u[lpf + st_goff[k]];
+        if constexpr (MODE == kFusedCG) {
+          f.p[k] = A.pold[lpf + st_goff[k]];
+          f.x[k] = A.x[lpf + st_goff[k]];
+        }
+      }
+    }
+    const int64_t lv = (in && cl + 1 <= ncx) ? static_cast<int64_t>(cl + 1) * A.vps : 0;
+#pragma unroll
+    for (int k = 0; k < NPV; ++k) f.v[k] = A.xv[lv + (v_off[k] >= 0 ? v_off[k] : 0)];
+    f.kc = kcp[(A.kc && in) ? static_cast<int64_t>(cl) * kc_ps + kc_cell : 0];
+  };
+  // s_waitcnt vmcnt(n), expcnt / lgkmcnt untouched (gfx9 encoding)
+  constexpr int kWaitNewest = 0x0F70 | (NLD & 15) | ((NLD >> 4) << 14);
+
+  auto layer = [&](int cx, PF& pfc, PF& pfn) __attribute__((always_inline)) {
     const int cur = (cx - cbeg) & 1, nxt = cur ^ 1;
     const bool last = (cx == cend - 1);   // end of this segment
     const bool glast = (cx == ncx - 1);   // end of the march
     const bool red = (cx < sa);           // redundant layer: carry only
     __syncthreads();
 
-    // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
+    // ---- prefetch: DEPTH 1 loads layer cx+1 into pfc (used at the end of
+    // this layer); DEPTH 2 loads layer cx+2 into pfn while pfc (layer cx+1,
+    // issued one layer ago) is still landing
     const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
-    T pf_r[NPF], pf_p[NPF], pf_x[NPF];
-    T pf_v[NPV];
-    // next layer's cell coefficient rides with the prefetch (a load consumed
-    // in the same layer would make the wave wait for the whole batch)
-    T kc_nxt = T(0);
-    if (A.kc && !last && cell_on) kc_nxt = A.kc[static_cast<int64_t>(cx + 1) * kc_ps + kc_cell];
-    // Unconditional loads (the last layer re-reads layer 0, unused): a
-    // per-slot conditional load makes the register allocator copy
-    // half-loaded pairs, and each copy waits for its load.
-    const int64_t lpf = last ? 0 : lnext;
-#pragma unroll
-    for (int k = 0; k < NPF; ++k) {
-      pf_r[k] = T(0);
-      pf_p[k] = T(0);
-      pf_x[k] = T(0);
-      if constexpr ((BDX_F4_DROP & 4) == 0) {
-        pf_r[k] = A.u[lpf + st_goff[k]];
-        if constexpr (MODE == kFusedCG) {
-          pf_p[k] = A.pold[lpf + st_goff[k]];
-          if (xupd) pf_x[k] = A.x[lpf + st_goff[k]];
-        }
-      }
+    if constexpr (DEPTH == 1) {
+      issue(pfc, cx + 1);
+    } else {
+      issue(pfn, cx + 2);
     }
-#pragma unroll
-    for (int k = 0; k < NPV; ++k) {
-      pf_v[k] = T(0);
-      if (!last && v_off[k] >= 0) pf_v[k] = A.xv[static_cast<int64_t>(cx + 2) * A.vps + v_off[k]];
-    }
+    T(&pf_r)[NPF] = pfc.r;
+    T(&pf_p)[NPF] = pfc.p;
+    T(&pf_x)[NPF] = pfc.x;
+    T(&pf_v)[NPV] = pfc.v;
 
     const T* __restrict__ su = s_u[cur];
     const T* __restrict__ sX = s_X[cur];
@@ -489,7 +510,10 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     // writes) drain while the next layer computes.  The wait is explicit and
     // unconditional (vmcnt(0) only; gfx9 encoding) so the waitcnt pass sees
     // no prefetch register pending on any path after this point.
-    __builtin_amdgcn_s_waitcnt(0x0F70);
+    if constexpr (DEPTH == 1)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    else
+      __builtin_amdgcn_s_waitcnt(kWaitNewest);  // pfc landed, pfn in flight
     if (!last) {
       T* __restrict__ un = s_u[nxt];
 #pragma unroll
@@ -528,7 +552,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         const int e = tid + k * NT;
         if (e < NV) s_X[nxt][NV + e] = pf_v[k];
       }
-      if (A.kc) s_kc[nxt][c] = kc_nxt;  // (the prefetch batch has landed here)
+      if (A.kc) s_kc[nxt][c] = cell_on ? pfc.kc : T(0);  // (the batch has landed here)
     }
 
     // ------------------------------------------------ gather-sum and write out
@@ -583,6 +607,12 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         }
       }
     }
+  };
+  PF pfa, pfb;
+  if constexpr (DEPTH == 2) issue(pfa, cbeg + 1);
+  for (int cx = cbeg; cx < cend; cx += 2) {
+    layer(cx, pfa, pfb);
+    if (cx + 1 < cend) layer(cx + 1, pfb, pfa);
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
@@ -613,11 +643,24 @@ inline int pack_tables4(int nd, int nq, const double* phi0, const double* Dd, co
   return kFusedTabMax;
 }
 
+// Prefetch depth of the x-march (layers in flight ahead of the one being
+// computed): BDX_F4_DEPTH=1|2 at run time (A/B), default 2.
+inline int fused4_depth() {
+  static const int d = [] {
+    const char* e = std::getenv("BDX_F4_DEPTH");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  return d;
+}
+
 template <int MODE>
 int launch_fused4(const Fused2Args<double>& a, const FusedTables<double>& tb, hipStream_t st) {
   constexpr int TY = BDX_F4_TY, TZ = BDX_F4_TZ;
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
-  lap_fused4_kernel<TY, TZ, MODE><<<nblk, TY * TZ * 16, 0, st>>>(a, tb);
+  if (fused4_depth() == 1)
+    lap_fused4_kernel<TY, TZ, MODE, 1><<<nblk, TY * TZ * 16, 0, st>>>(a, tb);
+  else
+    lap_fused4_kernel<TY, TZ, MODE, 2><<<nblk, TY * TZ * 16, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());
 }

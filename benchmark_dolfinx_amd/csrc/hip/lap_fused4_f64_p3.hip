@@ -62,8 +62,11 @@ extern "C" int bdx_fused4_segments(int tiles, int ncx) {
   int per_cu = 0, dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lap_fused4_kernel<TY, TZ, kFusedCG>,
-                                                   TY * TZ * 16, 0) != hipSuccess)
+      (fused4_depth() == 1
+           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                 &per_cu, lap_fused4_kernel<TY, TZ, kFusedCG, 1>, TY * TZ * 16, 0)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                 &per_cu, lap_fused4_kernel<TY, TZ, kFusedCG, 2>, TY * TZ * 16, 0)) != hipSuccess)
     return 1;
   return fused_choose_segments(tiles, ncx, per_cu * cus);
 }
