@@ -27,6 +27,7 @@ __device__ __forceinline__ int64_t row_base(const RowSpace& s, int64_t row) {
   return (i * s.L1 + j) * s.ld;
 }
 
+// Fused dot-product kernel: per-block partial sums of a.b (deterministic order).
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
     dot_rows_kernel(RowSpace s, const T* __restrict__ a, const T* __restrict__ b,

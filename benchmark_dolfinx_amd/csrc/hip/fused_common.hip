@@ -215,6 +215,7 @@ __global__ void reduce_partials_slices(const double* __restrict__ partials, int 
   if (threadIdx.x == 0) out[blockIdx.x] = t;
 }
 
+// Fixed-order sum of the per-tile p.Ap partials into one device scalar slot.
 __global__ void reduce_partials_fixed(const double* __restrict__ partials, int n,
                                       double* __restrict__ out, int slot) {
   __shared__ double lds[16];

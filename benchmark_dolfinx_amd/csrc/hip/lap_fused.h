@@ -199,6 +199,7 @@ struct FusedArgs {
   T kappa;
 };
 
+// fused (v1 family): stored or on-the-fly geometry, quadrature-point arrays in LDS.
 template <typename T, int ND, int NQ, int TY, int TZ, int GEOM, int MODE>
 __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
     lap_fused_kernel(FusedArgs<T> A, FusedTables<T> tb) {

@@ -80,6 +80,7 @@ struct Fused2Args {
   T kappa;
 };
 
+// fused2: x-march over (y, z) tiles with general (trilinear) or affine geometry.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
 __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
     lap_fused2_kernel(Fused2Args<T> A, FusedTables<T> tb) {

@@ -46,6 +46,7 @@
 #endif
 template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 2; };
 
+// fused3: fused2's march with direct collocation gradients and wave-local x passes.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
 __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
     lap_fused3_kernel(Fused2Args<T> A, FusedTables<T> tb) {

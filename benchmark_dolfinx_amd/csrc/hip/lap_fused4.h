@@ -76,6 +76,7 @@ __device__ __forceinline__ double f4_mat(const double* tab, int id, int r, int c
   return id == 3 ? tab[32 + c * 4 + r] : tab[id * 16 + r * 4 + c];
 }
 
+// fused4: MFMA (y, z) Kronecker core on parallelepiped Q3 cells, x-marching CG fusion.
 template <int TY, int TZ, int MODE, int DEPTH>
 __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     lap_fused4_kernel(Fused2Args<double> A, FusedTables<double> tb) {
@@ -644,11 +645,13 @@ inline int pack_tables4(int nd, int nq, const double* phi0, const double* Dd, co
 }
 
 // Prefetch depth of the x-march (layers in flight ahead of the one being
-// computed): BDX_F4_DEPTH=1|2 at run time (A/B), default 2.
+// computed): BDX_F4_DEPTH=1|2 at run time (A/B), default 1 (depth 2 measured
+// 1.2-1.5 % slower in an interleaved same-box A/B, Q3 300 M: 45.4/45.5 vs
+// 46.1/46.1 GDoF/s; the second register set costs occupancy headroom).
 inline int fused4_depth() {
   static const int d = [] {
     const char* e = std::getenv("BDX_F4_DEPTH");
-    return (e && std::atoi(e) == 1) ? 1 : 2;
+    return (e && std::atoi(e) == 2) ? 2 : 1;
   }();
   return d;
 }

@@ -1,6 +1,7 @@
 // Fused v4 operator kernels (MFMA core), double, degree 3.
 #include "lap_fused4.h"
 
+// fused4 apply entry (CG-fused or plain action) for Q3 FP64.
 extern "C" int bdx_fused4_apply_f64_p3(
     int mode, int affine_ok, const int64_t* latd, int nq, const double* wts, const double* qpts,
     const double* u, const double* pold, double* pnew, double* x, double* y, double* yb,
@@ -41,11 +42,13 @@ extern "C" int bdx_fused4_apply_f64_p3(
                           : launch_fused4<kFusedAction>(a, tb, st);
 }
 
+// Pack the 1D M / K / C tables of the quadrature rule for fused4.
 extern "C" int bdx_fused4_tables_f64(int nd, int nq, const double* phi0, const double* Dd,
                                      const double* wts, double* out) {
   return pack_tables4(nd, nq, phi0, Dd, wts, out);
 }
 
+// Cell tile (TY, TZ) of the fused4 instance, for the host-side launch geometry.
 extern "C" int bdx_fused4_tile(int* ty, int* tz) {
   *ty = BDX_F4_TY;
   *tz = BDX_F4_TZ;

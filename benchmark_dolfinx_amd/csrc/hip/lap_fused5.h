@@ -92,6 +92,7 @@ struct F5Shape {
   static constexpr int DZP = DZ | 1, PLP = DY * DZP;
 };
 
+// fused5: nodal x / z / y Kronecker passes for parallelepiped cells, P = 3..7.
 template <typename T, int ND, int NARR, int MODE>
 __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     lap_fused5_kernel(Fused2Args<T> A, const T* __restrict__ tabd) {

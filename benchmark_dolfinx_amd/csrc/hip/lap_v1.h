@@ -32,6 +32,7 @@ struct V1Shape {
   static constexpr int threads = ((cpb * nq3 + 63) / 64) * 64;
 };
 
+// v1: the reference algorithm (one cell per workgroup slot, quadrature-point arrays).
 template <typename T, int ND, int NQ, int MODE, int GEOM>
 __global__ void __launch_bounds__(V1Shape<NQ>::threads)
     lap_v1_kernel(BdxLattice lat, OpTables<T> tb, const T* __restrict__ G,

@@ -12,6 +12,7 @@
 
 namespace {
 
+// Stored geometry: G at every quadrature point in the reference layout.
 template <typename T, int NQ>
 __global__ void __launch_bounds__(256)
     geometry_kernel(BdxLattice lat, OpTables<T> tb, const T* __restrict__ xv,
@@ -71,6 +72,7 @@ int launch_geometry(int nq, const BdxLattice& lat, const OpTables<T>& tb,
   return static_cast<int>(hipGetLastError());
 }
 
+// Wave-per-row CSR SpMV (the reference's assembled-matrix comparison operator).
 template <typename T>
 __global__ void __launch_bounds__(256)
     spmv_kernel(int64_t nrows, const int64_t* __restrict__ row_ptr,

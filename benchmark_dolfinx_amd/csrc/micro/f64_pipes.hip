@@ -40,14 +40,17 @@ __device__ __forceinline__ double mfma_loop(int iters, double x) {
   return s[0] + s[1] + s[2] + s[3];
 }
 
+// FP64 VALU FMA throughput loop.
 __global__ void __launch_bounds__(512) k_valu(int it, double* out) {
   double r = valu_loop(it, threadIdx.x * 1e-3);
   if (r == 12345.0) out[0] = r;
 }
+// FP64 MFMA 16x16x4 throughput loop.
 __global__ void __launch_bounds__(512) k_mfma(int it, double* out) {
   double r = mfma_loop(it, threadIdx.x * 1e-3);
   if (r == 12345.0) out[0] = r;
 }
+// VALU waves and MFMA waves side by side (pipe sharing).
 __global__ void __launch_bounds__(512) k_mix(int itv, int itm, double* out) {
   double r;
   if (threadIdx.x < 256) r = valu_loop(itv, threadIdx.x * 1e-3);
@@ -89,14 +92,17 @@ __device__ __forceinline__ float mfma32_loop(int iters, float x) {
   f4 s = c0 + c1 + c2 + c3;
   return s[0] + s[1] + s[2] + s[3];
 }
+// FP32 packed-FMA throughput loop.
 __global__ void __launch_bounds__(512) k_valu32(int it, float* out) {
   float r = valu32_loop(it, threadIdx.x * 1e-3f);
   if (r == 12345.0f) out[0] = r;
 }
+// FP32 MFMA 16x16x4 throughput loop.
 __global__ void __launch_bounds__(512) k_mfma32(int it, float* out) {
   float r = mfma32_loop(it, threadIdx.x * 1e-3f);
   if (r == 12345.0f) out[0] = r;
 }
+// FP32 VALU and MFMA waves side by side.
 __global__ void __launch_bounds__(512) k_mix32(int itv, int itm, float* out) {
   float r;
   if (threadIdx.x < 256) r = valu32_loop(itv, threadIdx.x * 1e-3f);

@@ -124,7 +124,11 @@ def device_name(dev: int = 0) -> str:
     """hipDeviceProp name + gcnArchName (torch's get_device_name() returns a
     generic marketing string on this stack)."""
     info = device_info(dev)
-    fields = dict(line.strip().split(": ", 1) for line in info.splitlines() if ": " in line)
+    fields = {}
+    for line in info.splitlines():
+        key, sep, val = line.partition(":")
+        if sep:
+            fields[key.strip()] = val.strip()
     name = fields.get("Device", "unknown")
     arch = fields.get("gcnArch", "")
     return f"{name} ({arch})" if arch else name

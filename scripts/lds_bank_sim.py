@@ -8,7 +8,6 @@ For a candidate LDS layout (row pitch, block pitch, cell pitch in doubles) it
 counts the LDS cycles of one cell layer and the cycles lost to conflicts, so
 paddings can be chosen offline.   usage: python scripts/lds_bank_sim.py
 """
-import itertools
 from collections import defaultdict
 
 B128_GROUPS = [

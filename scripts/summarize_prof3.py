@@ -11,7 +11,8 @@ rows = list(csv.DictReader(open(d / "trace_kernel_stats.csv")))
 out.append("| kernel | calls | avg us | % |")
 out.append("|---|---|---|---|")
 for r in rows[:12]:
-    out.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.2f} |")
+    out.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
+               f"{float(r['Percentage']):.2f} |")
 for fam in ("lap_fused3_kernel", "cg_update_iface_kernel"):
     agg = collections.defaultdict(float)
     cnt = collections.Counter()

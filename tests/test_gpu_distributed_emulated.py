@@ -3,7 +3,6 @@ with RCCL semantics emulated (collectives reject host tensors), through the
 real bench.py `run()` and the CLI driver.  This is the rehearsal of the
 driver's torchrun N = 2/4/8 launches that cannot run on a 1-GPU box."""
 
-import argparse
 import os
 import sys
 

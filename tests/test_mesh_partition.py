@@ -2,7 +2,6 @@
 partition / halo tables (replaces ParMETIS + ghost_layer_mesh,
 src/mesh.cpp:26-114): pure-function property tests simulating R ranks."""
 
-import itertools
 
 import numpy as np
 import pytest
