@@ -63,6 +63,10 @@ def parse_args(argv=None):
                          "the config's DoF target")
     ap.add_argument("--profile-steps", type=int, default=5,
                     help="extra eager iterations with hipEvent phase timers (0: none)")
+    ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline run, time the same config with per-cell random "
+                         "coefficients and on the perturbed (general trilinear) mesh and report "
+                         "random_kappa_gdofs / general_gdofs (GPU platform only)")
     return ap.parse_args(argv)
 
 
@@ -100,14 +104,22 @@ def run(comm, a) -> dict | None:
                   flush=True)
 
     t_setup = time.perf_counter()
+    phase_t = {}
+
+    def mark(name):
+        phase_t[name] = time.perf_counter() - t_setup - sum(phase_t.values())
+
     log(f"mesh {nx} degree {degree} fp{bits} on {n} rank(s)")
     pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, a.perturb, a.kappa)
     log(f"problem built (partition {pb.lat.pgrid}, {pb.partition})")
+    mark("problem")
     u = pb.assemble_rhs()
     x = pb.new_vector()
     log("rhs assembled")
+    mark("rhs")
     op = make_operator(pb, a.kernel, a.geometry)
     log(f"operator {getattr(op, 'name', type(op).__name__)} ready")
+    mark("operator")
 
     def sync():
         if gpu:
@@ -125,6 +137,7 @@ def run(comm, a) -> dict | None:
         cg_solve(op, pb, x, u, a.warmup, 0.0)
     sync()
     log("warmup done")
+    mark("warmup")
     t_setup = time.perf_counter() - t_setup
     t0 = time.perf_counter()
     if gpu:
@@ -157,9 +170,23 @@ def run(comm, a) -> dict | None:
         phases_max = {k: max(p[k] for p in allp) for k in phases}
     if hasattr(op, "close"):
         op.close()
+    px, py, pz = pb.lat.pgrid
+    mesh_nx, ndofs_global = list(nx), pb.ndofs_global
+    kname = getattr(op, "name", type(op).__name__)
+    geom = getattr(op, "geometry", "otf")
+    del op, x, u, pb, rt
+    if gpu:
+        del cg
+        torch.cuda.empty_cache()
+    extras = {}
+    if gpu and a.extras in ("on", "auto"):
+        # the north-star variants of the same config (BASELINE.json: random
+        # coefficients; the reference's --geom_perturb_fact general cells)
+        for key, kappa, pert in (("random_kappa", "random", a.perturb),
+                                 ("general", a.kappa, a.perturb or 0.1)):
+            extras[key] = _variant(comm, a, nx, degree, dtype, kappa, pert, sync, log)
     if comm.rank != 0:
         return None
-    px, py, pz = pb.lat.pgrid
     return {
         "metric": "GDOF/s matrix-free Laplacian apply, Q3@300M & Q6@500M dofs/GPU, "
                   "1/2/4/8 MI355X",
@@ -177,26 +204,66 @@ def run(comm, a) -> dict | None:
                 "as the reference)",
         "config": {
             "model": f"Q{degree} Poisson, qmode=1 GLL, matrix-free CG",
-            "global_batch": pb.ndofs_global,
+            "global_batch": ndofs_global,
             "seq_len": degree,
             "parallelism": f"dd{n} ({px}x{py}x{pz} box partition)",
             "dofs_per_gpu": dpg,
-            "mesh": list(nx),
-            "kernel": getattr(op, "name", type(op).__name__),
-            "geometry": getattr(op, "geometry", "otf"),
+            "mesh": mesh_nx,
+            "kernel": kname,
+            "geometry": geom,
             "kappa": a.kappa,
             "geom_perturb_fact": a.perturb,
             "runtime": runtime,
             "per_gpu_gdofs": value / n,
             "y_norm": ynorm,
             "setup_s": t_setup,
+            "setup_phases_s": phase_t,
             "device": _device_name() if gpu else "cpu",
             "build_flags": flags,
             "comm": comm_info,
             "phases_ms": phases,
             "phases_ms_max_over_ranks": phases_max,
         },
+        "random_kappa_gdofs": extras.get("random_kappa", {}).get("value"),
+        "general_gdofs": extras.get("general", {}).get("value"),
+        "variants": extras,
     }
+
+
+def _variant(comm, a, nx, degree, dtype, kappa, perturb, sync, log) -> dict:
+    """Time one variant of the headline config (same mesh and degree) with
+    its own operator and CG; min(steps, 50) timed iterations after 3 warmup."""
+    import torch
+
+    from benchmark_dolfinx_amd.driver import make_operator
+    from benchmark_dolfinx_amd.models.poisson import PoissonProblem
+    from benchmark_dolfinx_amd.solvers.cg import DeviceCG
+
+    pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, perturb, kappa)
+    u = pb.assemble_rhs()
+    x = pb.new_vector()
+    op = make_operator(pb, a.kernel, a.geometry)
+    steps = min(a.steps, 50)
+    cg = DeviceCG(pb)
+    cg.start(op, x, u)
+    cg.iterate(3)
+    cg.wait()
+    sync()
+    t0 = time.perf_counter()
+    cg.iterate(steps)
+    cg.wait()
+    sync()
+    dt = comm.allreduce_scalar(time.perf_counter() - t0, "max")
+    rec = {"value": pb.ndofs_global * steps / (1e9 * dt), "ms_per_step": 1e3 * dt / steps,
+           "steps": steps, "kappa": kappa, "geom_perturb_fact": perturb,
+           "kernel": getattr(op, "name", type(op).__name__),
+           "geometry": getattr(op, "geometry", "otf"), "y_norm": pb.norm(x)}
+    log(f"variant kappa={kappa} perturb={perturb}: {rec['value']:.2f} GDoF/s ({rec['kernel']})")
+    if hasattr(op, "close"):
+        op.close()
+    del op, cg, x, u, pb
+    torch.cuda.empty_cache()
+    return rec
 
 
 def _device_name() -> str:
