@@ -45,10 +45,16 @@
 #define BDX_X3_NOSYNC 0
 #endif
 template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 2; };
+// Waves per SIMD the general (trilinear, AFF = 0) instances are compiled for:
+// at NQ = 5 the per-point geometry needs ~250 VGPRs, and forcing the default 3
+// waves spilled 159 dwords (Q3 general 7.7 GDoF/s vs 18.2 at 2 waves, same box)
+template <int NQ, int AFF> struct Fused3Waves {
+  static constexpr int value = AFF ? FusedWaves<NQ>::value : 2;
+};
 
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
-__global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), FusedWaves<NQ>::value)
+__global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fused3Waves<NQ, AFF>::value))
     lap_fused3_kernel(Fused2Args<T> A, FusedTables<T> tb) {
   using S = FusedShape<T, ND, NQ, TY, TZ>;
   constexpr int P = S::P, DY = S::DY, DZ = S::DZ, PL = DY * DZ;

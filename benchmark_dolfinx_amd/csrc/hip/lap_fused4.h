@@ -35,7 +35,7 @@
 #define BDX_F4_TZ 4
 #endif
 #ifndef BDX_F4_WAVES
-#define BDX_F4_WAVES 2
+#define BDX_F4_WAVES 3
 #endif
 // Timing-only phase drops for A/B attribution (wrong numerics when nonzero):
 // 1 = MFMA core, 2 = gather + write-out, 4 = next-layer global loads,
@@ -54,6 +54,16 @@
 #endif
 #ifndef BDX_F4_DROP
 #define BDX_F4_DROP 0
+#endif
+// 1: the per-lane x-factor rows live in LDS (read per layer, 32 fewer VGPRs)
+// instead of registers
+#ifndef BDX_F4_XLDS
+#define BDX_F4_XLDS 1
+#endif
+// 1: the gather-source descriptors (4 packed LDS offsets per output slot)
+// live in LDS instead of registers
+#ifndef BDX_F4_OLDS
+#define BDX_F4_OLDS 1
 #endif
 
 typedef double bdx_f64x4 __attribute__((ext_vector_type(4)));
@@ -110,6 +120,12 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   __shared__ T s_e[EB + 1];
   __shared__ T s_X[2][2 * NV];
   __shared__ T s_kc[2][CELLS];  // per-cell coefficient, double buffered
+#if BDX_F4_XLDS
+  __shared__ __attribute__((aligned(16))) T s_Xr[4 * 4 * ND];  // [m][xi][l]
+#endif
+#if BDX_F4_OLDS
+  __shared__ __attribute__((aligned(8))) int s_osrc[NOUT][NT][2];
+#endif
   __shared__ double s_red[16];
 
   const int tid = threadIdx.x;
@@ -155,11 +171,16 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   const int cy = c / TZ, cz = c % TZ;
   const bool cell_on = (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
   // this lane's rows X[xi][.] of the four x factors
+#if BDX_F4_XLDS
+  if (tid < 64) s_Xr[tid] = f4_mat(tab, tid >> 4, (tid >> 2) & 3, tid & 3);
+  const T* __restrict__ XrL = s_Xr + xi * ND;
+#else
   T Xr[4][ND];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int l = 0; l < ND; ++l) Xr[m][l] = f4_mat(tab, m, xi, l);
+#endif
 
   T beta = T(0), xalpha = T(0);
   const bool xupd = MODE == kFusedCG && A.xa_num >= 0;
@@ -227,11 +248,18 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     }
   }
   // ---- per-thread output descriptors (planes 0..P of a layer)
-  int o_src[NOUT][2], o_off[NOUT], o_meta[NOUT];
+#if BDX_F4_OLDS
+  int(*o_src)[NT][2] = s_osrc;
+#define BDX_F4_OSRC(k, h) o_src[k][tid][h]
+#else
+  int o_src[NOUT][2];
+#define BDX_F4_OSRC(k, h) o_src[k][h]
+#endif
+  int o_off[NOUT], o_meta[NOUT];
 #pragma unroll
   for (int k = 0; k < NOUT; ++k) {
     const int e = tid + k * NT;
-    o_src[k][0] = o_src[k][1] = ZSLOT | (ZSLOT << 16);
+    BDX_F4_OSRC(k, 0) = BDX_F4_OSRC(k, 1) = ZSLOT | (ZSLOT << 16);
     o_off[k] = 0;
     o_meta[k] = 0;
     if (e < ND * PL) {
@@ -247,8 +275,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         for (int ccy = cyl; ccy <= cyh; ++ccy)
           for (int ccz = czl; ccz <= czh; ++ccz)
             src[ns++] = (ccy * TZ + ccz) * PC + (ly - ccy * P) * P1 + (lz - ccz * P) * RP + pl;
-        o_src[k][0] = src[0] | (src[1] << 16);
-        o_src[k][1] = src[2] | (src[3] << 16);
+        BDX_F4_OSRC(k, 0) = src[0] | (src[1] << 16);
+        BDX_F4_OSRC(k, 1) = src[2] | (src[3] << 16);
         const int gy = y0 + ly, gz = z0 + lz;
         const bool iy = ly < oy, iz = lz < oz;
         int kind, off;
@@ -453,11 +481,18 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         for (int j = 0; j < ND; ++j) V[j] = uu[m][j];
         return;
       }
+#if BDX_F4_XLDS
+      const bdx_f64x2 x01 = *reinterpret_cast<const bdx_f64x2*>(XrL + m * 16);
+      const bdx_f64x2 x23 = *reinterpret_cast<const bdx_f64x2*>(XrL + m * 16 + 2);
+      const T xr[ND] = {x01[0], x01[1], x23[0], x23[1]};
+#else
+      const T(&xr)[ND] = Xr[m];
+#endif
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
         T s = T(0);
 #pragma unroll
-        for (int l = 0; l < ND; ++l) s += Xr[m][l] * uu[l][j];
+        for (int l = 0; l < ND; ++l) s += xr[l] * uu[l][j];
         V[j] = s;
       }
     };
@@ -566,8 +601,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         const int m = o_meta[k];
         if (!(m & kValid)) continue;
         const int pl = (m >> 8) & 15, rem = m >> 12;
-        T v = s_e[o_src[k][0] & 0xffff] + s_e[o_src[k][0] >> 16] +
-              s_e[o_src[k][1] & 0xffff] + s_e[o_src[k][1] >> 16];
+        const int os0 = BDX_F4_OSRC(k, 0), os1 = BDX_F4_OSRC(k, 1);
+        T v = s_e[os0 & 0xffff] + s_e[os0 >> 16] + s_e[os1 & 0xffff] + s_e[os1 >> 16];
         if (pl == 0) v += s_c[cur][rem];
         if (pl == P && !last) {
           s_c[nxt][rem] = v;
@@ -620,6 +655,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     // indexed by (tile, segment): invariant under any launch split
     if (tid == 0) A.partials[(ty * A.ntz + tz) * A.nseg + seg] = t;
   }
+#undef BDX_F4_OSRC
 }
 
 // 1D matrices of the quadrature rule (host, double): M1 = B^T W B,
