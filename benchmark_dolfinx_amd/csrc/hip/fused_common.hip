@@ -149,8 +149,8 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (v0 + u < nvp) {
-        vy[u] = *reinterpret_cast<const V*>(y + pbase + static_cast<int64_t>(v0 + u) * W);
-        vr[u] = *reinterpret_cast<const V*>(r + pbase + static_cast<int64_t>(v0 + u) * W);
+        vy[u] = ld_stream(reinterpret_cast<const V*>(y + pbase + static_cast<int64_t>(v0 + u) * W));
+        vr[u] = ld_stream(reinterpret_cast<const V*>(r + pbase + static_cast<int64_t>(v0 + u) * W));
       }
     }
 #pragma unroll
@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(256)
         vr[u][e] = rn;
         acc += static_cast<double>(rn) * static_cast<double>(rn);
       }
-      *reinterpret_cast<V*>(r + pbase + static_cast<int64_t>(v) * W) = vr[u];
+      st_stream(reinterpret_cast<V*>(r + pbase + static_cast<int64_t>(v) * W), vr[u]);
     }
   }
   const double t = block_sum(acc, lds);

@@ -375,10 +375,10 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       f.p[k] = T(0);
       f.x[k] = T(0);
       if constexpr ((BDX_F4_DROP & 4) == 0) {
-        f.r[k] = A.u[lpf + st_goff[k]];
+        f.r[k] = ld_stream(A.u + lpf + st_goff[k]);
         if constexpr (MODE == kFusedCG) {
-          f.p[k] = A.pold[lpf + st_goff[k]];
-          f.x[k] = A.x[lpf + st_goff[k]];
+          f.p[k] = ld_stream(A.pold + lpf + st_goff[k]);
+          f.x[k] = ld_stream(A.x + lpf + st_goff[k]);
         }
       }
     }
@@ -618,8 +618,10 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
           if (kind == 0) continue;  // Dirichlet y was written at staging
           v = T(0);
         }
-        T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
-        dst[o_off[k]] = v;
+        if (kind == 0)
+          st_stream(ybase[0] + o_off[k], v);
+        else
+          (kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3])[o_off[k]] = v;
       }
     }
 
@@ -633,8 +635,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         if (tid + k * NT < P * PL && (m & kValid) && (m & kOwnT)) {
           const int gxx = (cx + 1) * P + ((m >> 4) & 15);
           if constexpr (MODE == kFusedCG) {
-            pnl[st_goff[k]] = pf_r[k];
-            if (xupd) A.x[lnext + st_goff[k]] = pf_x[k];
+            st_stream(pnl + st_goff[k], pf_r[k]);
+            if (xupd) st_stream(A.x + lnext + st_goff[k], pf_x[k]);
           }
           if ((m & kBcYZ) || gxx == A.bcx_hi) {
             const bool rown = (m & kRownYZ) && gxx < A.ownx;

@@ -370,10 +370,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
       pf_p[k] = T(0);
       pf_x[k] = T(0);
       if (!(BDX_F5_DROP & 4) && !last && (st_meta[k] & kValid)) {
-        pf_r[k] = un_r[st_goff[k]];
+        pf_r[k] = ld_stream(un_r + st_goff[k]);
         if constexpr (MODE == kFusedCG) {
-          pf_p[k] = un_p[st_goff[k]];
-          if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = un_x[st_goff[k]];
+          pf_p[k] = ld_stream(un_p + st_goff[k]);
+          if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = ld_stream(un_x + st_goff[k]);
         }
       }
     }
@@ -553,8 +553,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
           if (kind == 0) continue;  // Dirichlet y was written at staging
           v = T(0);
         }
-        T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
-        dst[o_off[k]] = v;
+        if (kind == 0)
+          st_stream(ybase[0] + o_off[k], v);
+        else
+          (kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3])[o_off[k]] = v;
       }
     }
 
@@ -581,8 +583,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
             }
             if constexpr (MODE == kFusedCG) {
               if (m & kOwnT) {
-                pnl[st_goff[k]] = val;
-                if (xupd) un_x[st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
+                st_stream(pnl + st_goff[k], val);
+                if (xupd) st_stream(un_x + st_goff[k], pf_x[k] + xalpha * pf_p[k]);
               }
             }
             if ((m & kBcYZ) || gxx == A.bcx_hi) {
