@@ -54,6 +54,10 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
             auto = ("fused4" if fused_supported(pb, 4) else
                     "fused5" if fused_supported(pb, 5) else "fused3")
             kernel = os.environ.get("BDX_AUTO_AFFINE", auto)
+    if kernel == "dofmap":
+        # the unstructured data model: explicit cell->dof / cell->vertex maps
+        from .models.unstructured import DofmapLaplacianGPU
+        return DofmapLaplacianGPU(pb, "stored" if geometry == "stored" else "otf")
     if kernel == "fused5":
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 5) and geometry in ("auto", "otf"):

@@ -1,0 +1,161 @@
+"""Unstructured (dofmap) data model and its GPU operator.
+
+The reference stores a mesh the DOLFINx way: an explicit cell -> dof map, a
+cell -> geometry-node map with node coordinates, per-dof boundary markers and
+(for the GPU operator) per-quadrature-point geometry G, and it applies the
+operator through that indirection (src/laplacian.hpp:105-114,
+src/laplacian_gpu.hpp:153-170, built from the mesh in src/mesh.cpp:87-102;
+interior / boundary cell lists for the overlapped schedule,
+src/laplacian.hpp:215-272 and :281-349).
+
+`UnstructuredMesh` is that representation.  `from_problem` builds it for the
+benchmark's box (the lattice is only used to *construct* the arrays); nothing
+downstream assumes a lattice, so any hexahedral mesh, cell order or dof
+numbering can be fed in (`renumbered` applies arbitrary permutations and the
+tests check the operator is equivariant under them).  `DofmapLaplacianGPU`
+runs the `lap_dofmap` HIP kernel (csrc/hip/lap_dofmap.h): the v1 sum-
+factorisation core behind the dofmap gather and an atomic scatter-add, with
+the same interior-then-boundary overlap of the forward halo exchange as the
+reference.  Vectors keep the problem's storage layout, so the halo machinery
+and the CG solvers are shared with the structured operators.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..utils.timing import timed
+
+
+@dataclass
+class UnstructuredMesh:
+    cell_dofs: np.ndarray        # int32 [ncells, nd^3], tensor-product order (i, j, k)
+    cell_verts: np.ndarray       # int32 [ncells, 8], v = 4a + 2b + c
+    coords: np.ndarray           # [nverts, 3] geometry nodes
+    dof_flags: np.ndarray        # uint8 [ndofs]: bit 0 Dirichlet, bit 1 owned
+    interior_cells: np.ndarray   # int32: cells touching no ghost dof
+    boundary_cells: np.ndarray   # int32: the rest (computed after the halo arrives)
+    kc: np.ndarray | None        # per-cell coefficient or None (constant kappa)
+    degree: int
+
+    @property
+    def ncells(self) -> int:
+        return int(self.cell_dofs.shape[0])
+
+    @property
+    def ndofs(self) -> int:
+        return int(self.dof_flags.shape[0])
+
+    @classmethod
+    def from_problem(cls, pb) -> "UnstructuredMesh":
+        """The dofmap arrays of the problem's local box (cell id = the
+        lexicographic cell index of the lattice, dof id = the storage index)."""
+        lat = pb.lat
+        P, nd = lat.degree, lat.degree + 1
+        n0, n1, n2 = lat.n
+        L1, ld = lat.L[1], lat.ld
+        cx, cy, cz = np.meshgrid(np.arange(n0, dtype=np.int64), np.arange(n1, dtype=np.int64),
+                                 np.arange(n2, dtype=np.int64), indexing="ij")
+        cx, cy, cz = cx.ravel(), cy.ravel(), cz.ravel()
+        nc = cx.size
+        cdofs = np.empty((nc, nd ** 3), dtype=np.int32)
+        for i in range(nd):
+            for j in range(nd):
+                for k in range(nd):
+                    cdofs[:, (i * nd + j) * nd + k] = (((cx * P + i) * L1 + cy * P + j) * ld
+                                                       + cz * P + k)
+        cverts = np.empty((nc, 8), dtype=np.int32)
+        for v in range(8):
+            a, b, c = v >> 2, (v >> 1) & 1, v & 1
+            cverts[:, v] = ((cx + a) * (n1 + 1) + cy + b) * (n2 + 1) + cz + c
+        flags = np.zeros(lat.shape, dtype=np.uint8)
+        L = lat.L
+        flags[:L[0], :L[1], :L[2]] = (lat.bc_mask().astype(np.uint8)
+                                      | (lat.owned_mask().astype(np.uint8) << 1))
+        hi = [m - g for m, g in zip(lat.n, lat.gh)]
+        inner = (cx < hi[0]) & (cy < hi[1]) & (cz < hi[2])
+        ids = np.arange(nc, dtype=np.int32)
+        return cls(cdofs, cverts, np.ascontiguousarray(pb.xv_host.reshape(-1, 3)),
+                   flags.ravel(), ids[inner], ids[~inner],
+                   None if pb.kc is None else np.ascontiguousarray(pb.kc_host.reshape(-1)), P)
+
+    def renumbered(self, dof_perm: np.ndarray | None = None,
+                   cell_perm: np.ndarray | None = None,
+                   vert_perm: np.ndarray | None = None) -> "UnstructuredMesh":
+        """The same mesh with dof i renamed dof_perm[i], cell c stored at row
+        position where cell_perm[pos] = c, vertex v renamed vert_perm[v]."""
+        cd, cv, co, fl, kc = self.cell_dofs, self.cell_verts, self.coords, self.dof_flags, self.kc
+        inner, outer = self.interior_cells, self.boundary_cells
+        if dof_perm is not None:
+            cd = dof_perm[cd].astype(np.int32)
+            fl = np.empty_like(fl)
+            fl[dof_perm] = self.dof_flags
+        if vert_perm is not None:
+            cv = vert_perm[cv].astype(np.int32)
+            co = np.empty_like(co)
+            co[vert_perm] = self.coords
+        if cell_perm is not None:
+            pos = np.empty_like(cell_perm)
+            pos[cell_perm] = np.arange(cell_perm.size)
+            cd, cv = cd[cell_perm], cv[cell_perm]
+            kc = None if kc is None else kc[cell_perm]
+            inner, outer = np.sort(pos[inner]).astype(np.int32), np.sort(pos[outer]).astype(np.int32)
+        return UnstructuredMesh(np.ascontiguousarray(cd), np.ascontiguousarray(cv),
+                                np.ascontiguousarray(co), fl, inner, outer,
+                                None if kc is None else np.ascontiguousarray(kc), self.degree)
+
+
+class DofmapLaplacianGPU:
+    """Matrix-free stiffness operator on the unstructured data model.
+
+    geometry="otf": G per quadrature point from the cell's 8 geometry nodes;
+    "stored": G precomputed once per (cell, point) in the reference layout
+    [cell][6][nq^3] (src/geometry_gpu.hpp:26-132).
+    """
+
+    name = "dofmap"
+
+    def __init__(self, problem, geometry: str = "otf", mesh: UnstructuredMesh | None = None):
+        if problem.platform != "gpu":
+            raise ValueError("DofmapLaplacianGPU needs the GPU platform")
+        if geometry not in ("otf", "stored"):
+            raise ValueError(f"unknown geometry mode {geometry}")
+        self.pb = problem
+        self.k = problem.kernels
+        self.geometry = f"dofmap-{geometry}"
+        with timed("~setup dofmap"):
+            self.mesh = mesh or UnstructuredMesh.from_problem(problem)
+            dev, dt = problem.device, problem.dtype
+            m = self.mesh
+            self.cdofs = torch.from_numpy(m.cell_dofs).to(dev)
+            self.cverts = torch.from_numpy(m.cell_verts).to(dev)
+            self.coords = torch.from_numpy(m.coords).to(dev, dt)
+            self.flags = torch.from_numpy(m.dof_flags).to(dev)
+            self.inner = torch.from_numpy(m.interior_cells).to(dev)
+            self.outer = torch.from_numpy(m.boundary_cells).to(dev)
+            self.kc = None if m.kc is None else torch.from_numpy(m.kc).to(dev, dt)
+            self.G = None
+            self.geom = 1
+            if geometry == "stored":
+                nq3 = problem.tables.nq ** 3
+                self.G = torch.empty(m.ncells * 6 * nq3, dtype=dt, device=dev)
+                self.k.dofmap_geometry(m.ncells, self.cverts, self.coords, self.G)
+                self.geom = 0
+
+    def _run(self, cells, u, y):
+        n = int(cells.numel())
+        if n:
+            self.k.dofmap_apply(self.geom, cells, n, self.cdofs, self.cverts, self.coords,
+                                self.flags, self.G, self.pb.kappa, self.kc, u, y)
+
+    def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
+        pb = self.pb
+        y.zero_()
+        work = pb.halo.forward_begin(u)
+        self._run(self.inner, u, y)      # overlaps the forward exchange
+        pb.halo.forward_end(u, work)
+        self._run(self.outer, u, y)
+        pb.halo.reverse(y)

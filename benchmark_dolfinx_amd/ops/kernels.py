@@ -70,6 +70,20 @@ class HipKernels:
                                        ptr(G), ptr(xv), kappa, ptr(kc), ptr(u), ptr(y), ptr(lo),
                                        ptr(hi), _stream()), "v1_apply")
 
+    def dofmap_apply(self, geom: int, cells, ncl: int, cdofs, cverts, coords, flags, G,
+                     kappa: float, kc, u, y):
+        t, P = self.t, self.lat.degree
+        _check(self._f("bdx_dofmap_apply")(P, t.nq, geom, ptr(t.phi0), ptr(t.dphi1), ptr(t.wts),
+                                           ptr(t.qpts), t.identity, ptr(cells), ncl, ptr(cdofs),
+                                           ptr(cverts), ptr(coords), ptr(flags), ptr(G), kappa,
+                                           ptr(kc), ptr(u), ptr(y), _stream()), "dofmap_apply")
+
+    def dofmap_geometry(self, ncells: int, cverts, coords, G):
+        t, P = self.t, self.lat.degree
+        _check(self._f("bdx_dofmap_geometry")(P, t.nq, ptr(t.phi0), ptr(t.dphi1), ptr(t.wts),
+                                              ptr(t.qpts), ncells, ptr(cverts), ptr(coords),
+                                              ptr(G), _stream()), "dofmap_geometry")
+
     def geometry(self, xv, G):
         t = self.t
         _check(self._f("bdx_geometry")(ptr(self.latd), t.nq, ptr(t.phi0), ptr(t.dphi1),
