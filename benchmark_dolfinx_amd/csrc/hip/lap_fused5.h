@@ -38,6 +38,8 @@
 // x update, Dirichlet identity rows, p.Ap partials as element dots) and the
 // atomic-free gather with tile-interface buffers -- is fused4's.
 #pragma once
+#include <cstdlib>
+
 #include "lap_fused2.h"
 
 #ifndef BDX_F5_WAVES
@@ -70,7 +72,9 @@ template <> struct F5Tile<7, 2> { static constexpr int CPW = 1, TY = BDX_F5_TY7,
 template <> struct F5Tile<7, 4> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 template <int NARR> struct F5Tile<8, NARR> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 
-template <typename T, int ND, int NARR>
+// MFMA core (MF = 1, axis-aligned 2-array instance, one cell per wave):
+// per-wave buffer holds Kx u, Mx u (2 ND^3) and zM, zK (2 ND^3)
+template <typename T, int ND, int NARR, int MF = 0>
 struct F5Shape {
   static constexpr int P = ND - 1;
   static constexpr int CPW = F5Tile<ND, NARR>::CPW, TY = F5Tile<ND, NARR>::TY,
@@ -87,16 +91,43 @@ struct F5Shape {
   // element vectors for the gather: E[cell][j][k][i]
   static constexpr int RP = ND, P1 = ND * ND, PC = ND * ND * ND;
   static constexpr int WB0 = NARR * ARR;
-  static constexpr int WB = WB0 > CPW * PC ? WB0 : CPW * PC;  // per-wave buffer
+  static constexpr int WB1 = WB0 > CPW * PC ? WB0 : CPW * PC;
+  static constexpr int WB = (MF && 4 * PC > WB1) ? 4 * PC : WB1;  // per-wave buffer
   static constexpr int DY = TY * P + 1, DZ = TZ * P + 1, PL = DY * DZ;
   static constexpr int DZP = DZ | 1, PLP = DY * DZP;
 };
 
+// MFMA 16x16x4 in both precisions (cdna_hip_programming.md §3): A[m][k] at
+// lane m + 16k, B[k][n] at lane n + 16k (one value per lane); D[m][n] at
+// lane n + 16 g, register r with m = 4g + r (f32) or m = g + 4r (f64).
+template <typename T> struct F5Mfma;
+template <> struct F5Mfma<float> {
+  typedef float V4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ V4 mma(float a, float b, V4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __host__ __device__ constexpr int row(int g, int r) { return 4 * g + r; }
+};
+template <> struct F5Mfma<double> {
+  typedef double V4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ V4 mma(double a, double b, V4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+  static __host__ __device__ constexpr int row(int g, int r) { return g + 4 * r; }
+};
+
 // fused5: nodal x / z / y Kronecker passes for parallelepiped cells, P = 3..7.
-template <typename T, int ND, int NARR, int MODE>
-__global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
+// MF = 1 (axis-aligned cells, ND >= 6): the three passes as MFMA GEMMs with
+// the stacked 1D matrices as constant A operands (no scalar table loads):
+//   x: [K; M] (16 x 8) . u[l][(j, k)]                -> Kx u, Mx u
+//   z: [M; K] . (Kx u)[k][(i, j)], [K; M] . (Mx u)    -> zM = G00 Mz Kx u + G22 Kz Mx u,
+//                                                        zK = G11 Mz Mx u (same lanes)
+//   y: [My | Ky] (16 x 16) . [zM; zK][(j', arr)][(i, k)] -> y_e
+template <typename T, int ND, int NARR, int MODE, int MF = 0>
+__global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     lap_fused5_kernel(Fused2Args<T> A, const T* __restrict__ tabd) {
-  using S = F5Shape<T, ND, NARR>;
+  using S = F5Shape<T, ND, NARR, MF>;
+  static_assert(!MF || (NARR == 2 && S::CPW == 1 && ND <= 8), "MFMA core: 2-array, one cell per wave");
   constexpr int P = S::P, CPW = S::CPW, TY = S::TY, TZ = S::TZ;
   constexpr int DY = S::DY, DZ = S::DZ, PL = S::PL, DZP = S::DZP, PLP = S::PLP;
   constexpr int NT = S::NT, ND2 = ND * ND, NDP = S::NDP, ARR = S::ARR, WB = S::WB;
@@ -150,7 +181,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
   const int la = ab / ND, lb = ab % ND;
   const int c = wv * CPW + cw;
   const int cy = c / TZ, cz = c % TZ;
-  const bool cell_on = lane_on && (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
+  // MF: every lane of the wave works on its cell (the MFMA lane maps use all 64)
+  const bool cell_on = (MF || lane_on) && (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
   T* const Wb = s_w + wv * WB;             // this wave's buffer
   T* const Wc = Wb + cw * ND2 * NDP;       // this cell's rows of array 0
 
@@ -328,6 +360,24 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
   // Row a's pointer is laundered through an asm that consumes the result of
   // row a - 2 (d2): the scalar loads run one row ahead of the FMAs and at
   // most two rows are live in SGPRs.
+  // MFMA A operands (lane m + 16k holds A[m][k]): [K; M], [M; K] over k-steps
+  // of 4, and [My | Ky] (16 x 16) over 4 k-steps
+  T aKM[2] = {T(0), T(0)}, aMK[2] = {T(0), T(0)}, aY[4] = {T(0), T(0), T(0), T(0)};
+  if constexpr (MF) {
+    const int am = lane & 15, ak = lane >> 4;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int l = 4 * st + ak, rr = am & 7;
+      const T k_ = tabd[64 + rr * kF5Stride + l], m_ = tabd[rr * kF5Stride + l];
+      aKM[st] = am < 8 ? k_ : m_;
+      aMK[st] = am < 8 ? m_ : k_;
+    }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int kap = 4 * st + ak, id = kap >> 3, c_ = kap & 7;
+      aY[st] = am < 8 ? tabd[id * 64 + am * kF5Stride + c_] : T(0);
+    }
+  }
   T d1 = T(0), d2 = T(0);
   auto matvec = [&](int id, const T (&in)[ND], T (&out)[ND], T s, bool acc) {
 #pragma unroll
@@ -420,8 +470,107 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
     (void)G02;
     (void)G12;
 
-    // ------------------------------------------------ x pass: lane (j, k) = (la, lb)
     const T* __restrict__ ucell = su + (cy * P) * DZP + cz * P;
+    if constexpr (MF) {
+      using MM = F5Mfma<T>;
+      using V4 = typename MM::V4;
+      constexpr int ND2 = ND * ND, ND3 = ND2 * ND;
+      constexpr int ZT = sizeof(T) == 8 ? 2 : 4;  // z-pass tiles per group
+      const int n16 = lane & 15, g4 = lane >> 4;
+      T* const Wx = Wb;             // Kx u, Mx u: [arr][i][j][k]
+      T* const Wz = Wb + 2 * ND3;   // zM, zK:     [arr][i][j][k]
+      // ---- x pass: D[(arr, i)][(j, k)] = [K; M][(arr, i)][l] u[l][(j, k)]
+      V4 ax[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ax[t] = V4{0, 0, 0, 0};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int l = 4 * st + g4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int n = 16 * t + n16;
+          const bool ok = n < ND2 && l < ND;
+          const T b = ok ? ucell[l * PLP + (n / ND) * DZP + n % ND] : T(0);
+          ax[t] = MM::mma(aKM[st], b, ax[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = 16 * t + n16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = MM::row(g4, r);
+          if (n < ND2 && (m & 7) < ND) Wx[(m >> 3) * ND3 + (m & 7) * ND2 + n] = ax[t][r];
+        }
+      }
+      wave_sync();
+      // ---- z pass: columns (i, j), contraction over k; two tiles at a time
+      // (4 accumulators live: the FP64 instance otherwise spills)
+#pragma unroll
+      for (int h = 0; h < 4; h += ZT) {
+        V4 z1[ZT], z2[ZT];
+#pragma unroll
+        for (int t = 0; t < ZT; ++t) z1[t] = z2[t] = V4{0, 0, 0, 0};
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int k = 4 * st + g4;
+#pragma unroll
+          for (int t = 0; t < ZT; ++t) {
+            const int n = 16 * (h + t) + n16;
+            const bool ok = n < ND2 && k < ND;
+            const T b1 = ok ? Wx[n * ND + k] : T(0);
+            const T b2 = ok ? Wx[ND3 + n * ND + k] : T(0);
+            z1[t] = MM::mma(aMK[st], b1, z1[t]);
+            z2[t] = MM::mma(aKM[st], b2, z2[t]);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < ZT; ++t) {
+          const int n = 16 * (h + t) + n16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = MM::row(g4, r);
+            const T v = m < 8 ? G00 * z1[t][r] + G22 * z2[t][r] : G11 * z2[t][r];
+            if (n < ND2 && (m & 7) < ND) Wz[(m >> 3) * ND3 + n * ND + (m & 7)] = v;
+          }
+        }
+      }
+      wave_sync();
+      // ---- y pass: columns (i, k), contraction over (arr, j')
+      V4 ya[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ya[t] = V4{0, 0, 0, 0};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int kap = 4 * st + g4, arr = kap >> 3, jp = kap & 7;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int n = 16 * t + n16;
+          const bool ok = n < ND2 && jp < ND;
+          const T b = ok ? Wz[arr * ND3 + (n / ND) * ND2 + jp * ND + n % ND] : T(0);
+          ya[t] = MM::mma(aY[st], b, ya[t]);
+        }
+      }
+      // element dot and element vector E[j][k][i] (Wx is dead: E overlays it)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = 16 * t + n16;
+        const int i = n / ND, kq = n % ND;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = MM::row(g4, r);
+          if (n < ND2 && j < ND) {
+            const T ye = ya[t][r];
+            if constexpr (MODE == kFusedCG) {
+              if (cell_on && !red)
+                pap += static_cast<double>(ucell[i * PLP + j * DZP + kq]) * static_cast<double>(ye);
+            }
+            Wb[j * ND2 + kq * ND + i] = cell_on ? ye : T(0);
+          }
+        }
+      }
+    } else {
+    // ------------------------------------------------ x pass: lane (j, k) = (la, lb)
     {
       T u[ND];
 #pragma unroll
@@ -523,6 +672,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), BDX_F5_WAVES)
       T* eo = Wb + cw * PC + lb * RP + la;
 #pragma unroll
       for (int j = 0; j < ND; ++j) eo[j * P1] = cell_on ? ye[j] : T(0);
+    }
     }
     __syncthreads();
 
@@ -648,10 +798,31 @@ inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, co
 
 // affine_ok: 0 = general cells (refused), 1 = parallelepipeds, 2 = axis-aligned
 // boxes (diagonal Jacobians: the 2-array instance)
+// MFMA core for the axis-aligned instances with one cell per wave (ND >= 6):
+// BDX_F5_MFMA=1|0 at launch time (A/B and tests; a captured graph keeps the
+// instance it was captured with).  Default off: same-box A/B at Q6 500 M,
+// MFMA vs VALU core, FP32 55.2 vs 59.9 GDoF/s, FP64 33.8 vs 45.9 (the FP64
+// instance spills 28 dwords); PMC: scalar loads 3.4e8 -> 4e5, LDS
+// instructions 1.7e8 -> 3.0e8 (element-granular operand staging), waits
+// +60 % (profiles/r2_fused5_mfma.md).
+#ifndef BDX_F5_MFMA_DEFAULT
+#define BDX_F5_MFMA_DEFAULT 0
+#endif
+inline bool fused5_mfma() {
+  const char* e = std::getenv("BDX_F5_MFMA");
+  return e ? std::atoi(e) != 0 : BDX_F5_MFMA_DEFAULT != 0;
+}
+
 template <typename T, int ND, int MODE>
 int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStream_t st) {
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
+  if constexpr (ND >= 6) {
+    if (affine_ok == 2 && fused5_mfma()) {
+      lap_fused5_kernel<T, ND, 2, MODE, 1><<<nblk, F5Shape<T, ND, 2, 1>::NT, 0, st>>>(a, tabd);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   if (affine_ok == 2)
     lap_fused5_kernel<T, ND, 2, MODE><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
   else
