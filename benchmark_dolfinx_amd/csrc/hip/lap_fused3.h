@@ -48,8 +48,11 @@ template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 
 // Waves per SIMD the general (trilinear, AFF = 0) instances are compiled for:
 // at NQ = 5 the per-point geometry needs ~250 VGPRs, and forcing the default 3
 // waves spilled 159 dwords (Q3 general 7.7 GDoF/s vs 18.2 at 2 waves, same box)
+#ifndef BDX_FUSED3_GWAVES
+#define BDX_FUSED3_GWAVES 2
+#endif
 template <int NQ, int AFF> struct Fused3Waves {
-  static constexpr int value = AFF ? FusedWaves<NQ>::value : 2;
+  static constexpr int value = AFF ? FusedWaves<NQ>::value : BDX_FUSED3_GWAVES;
 };
 
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
