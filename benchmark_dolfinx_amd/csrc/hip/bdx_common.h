@@ -21,6 +21,22 @@ constexpr int kFusedTabMax = 2 * 9 * 12 + 9 * 8 + 8 * 12;
 
 enum { kGeomStored = 0, kGeomOTF = 1 };
 
+// Debug builds (BDX_DEBUG=1: `python -m benchmark_dolfinx_amd.ops.build
+// --variant debug=-DBDX_DEBUG=1`, loaded with BDX_HIP_LIB) turn on
+// device-side checks of the operator kernels' LDS and global index paths; a
+// failing check prints the expression and aborts the process (HIP device
+// assert) instead of reading or writing out of bounds.  Release builds compile
+// them out.
+#ifndef BDX_DEBUG
+#define BDX_DEBUG 0
+#endif
+#if BDX_DEBUG
+#include <cassert>
+#define BDX_DASSERT(c) assert(c)
+#else
+#define BDX_DASSERT(c) ((void)0)
+#endif
+
 // Streamed vectors (read or written once per CG iteration; every vector is
 // far larger than the 256 MiB Infinity Cache): BDX_NT bit 1 = non-temporal
 // loads, bit 2 = non-temporal stores.  Default 0: non-temporal loads AND

@@ -47,6 +47,7 @@ __global__ void __launch_bounds__(V1Shape<NQ>::threads)
   unsigned f = 0;
   if (is_dof) {
     dof = cdofs[cell * ND3 + (qx * ND + qy) * ND + qz];
+    BDX_DASSERT(dof >= 0);
     f = flags[dof];
   }
   const bool bc = f & 1u;

@@ -576,6 +576,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
           pap += (bcn && rown) ? static_cast<double>(val) * static_cast<double>(val) : 0.0;
         }
         const T v = ((m & kValid) && !bcn) ? val : T(0);
+        BDX_DASSERT(tid + k * NT >= P * PL || ((m >> 8) >= 0 && (m >> 8) < ND * PLP));
         if (tid + k * NT < P * PL) un[m >> 8] = v;
       }
 #pragma unroll
@@ -602,6 +603,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         if (!(m & kValid)) continue;
         const int pl = (m >> 8) & 15, rem = m >> 12;
         const int os0 = BDX_F4_OSRC(k, 0), os1 = BDX_F4_OSRC(k, 1);
+        BDX_DASSERT((os0 & 0xffff) <= ZSLOT && (os0 >> 16) <= ZSLOT && (os1 & 0xffff) <= ZSLOT &&
+                    (os1 >> 16) <= ZSLOT && rem < PL);
         T v = s_e[os0 & 0xffff] + s_e[os0 >> 16] + s_e[os1 & 0xffff] + s_e[os1 >> 16];
         if (pl == 0) v += s_c[cur][rem];
         if (pl == P && !last) {
@@ -618,6 +621,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
           if (kind == 0) continue;  // Dirichlet y was written at staging
           v = T(0);
         }
+        BDX_DASSERT(o_off[k] >= 0 && (kind != 0 || o_off[k] < (P + 1) * A.ps));
         if (kind == 0)
           st_stream(ybase[0] + o_off[k], v);
         else

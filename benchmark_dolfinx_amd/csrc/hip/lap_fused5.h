@@ -686,6 +686,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
         const int m = o_meta[k];
         if (!(m & kValid)) continue;
         const int pl = (m >> 8) & 15, rem = m >> 12;
+        BDX_DASSERT((o_src[k][0] & 0xffff) <= ZSLOT && (o_src[k][0] >> 16) <= ZSLOT &&
+                    (o_src[k][1] & 0xffff) <= ZSLOT && (o_src[k][1] >> 16) <= ZSLOT && rem < PL);
         T v = s_w[o_src[k][0] & 0xffff] + s_w[o_src[k][0] >> 16] +
               s_w[o_src[k][1] & 0xffff] + s_w[o_src[k][1] >> 16];
         if (pl == 0) v += s_c[cur][rem];
@@ -703,6 +705,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
           if (kind == 0) continue;  // Dirichlet y was written at staging
           v = T(0);
         }
+        BDX_DASSERT(o_off[k] >= 0 && (kind != 0 || o_off[k] < (P + 1) * A.ps));
         if (kind == 0)
           st_stream(ybase[0] + o_off[k], v);
         else
@@ -749,6 +752,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
             }
             v = val;
           }
+          BDX_DASSERT((m >> 8) >= 0 && (m >> 8) < ND * PLP);
           un[m >> 8] = v;
         }
       }

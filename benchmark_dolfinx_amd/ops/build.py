@@ -67,19 +67,31 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build failed: {cmd[0]} ... {cmd[-1]}")
 
 
-def build_host(force: bool = False) -> Path:
+HOST_SAN_SO = HERE / "libbdx_host_san.so"
+SAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+             "-fno-sanitize-recover=undefined"]
+
+
+def build_host(force: bool = False, sanitize: bool = False) -> Path:
+    """libbdx_host.so; with `sanitize`, libbdx_host_san.so built with
+    AddressSanitizer + UndefinedBehaviorSanitizer (host code only: load it with
+    BDX_HOST_LIB and LD_PRELOAD=libasan.so, see tests/test_host_sanitizers.py)."""
     srcs = _sources("host", ".cpp")
     flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-march=x86-64-v2",
              "-Wall", "-Wno-unknown-pragmas"]
+    out = HOST_SO
+    if sanitize:
+        flags = [f for f in flags if f != "-O3"] + SAN_FLAGS
+        out = HOST_SAN_SO
     digest = _digest(srcs + _headers(), " ".join(flags))
-    if not force and _up_to_date(HOST_SO, digest):
-        return HOST_SO
+    if not force and _up_to_date(out, digest):
+        return out
     cxx = shutil.which("g++") or "c++"
-    tmp = HOST_SO.with_suffix(".so.tmp")
+    tmp = out.with_suffix(".so.tmp")
     _run([cxx, *flags, "-I", str(CSRC / "include"), *map(str, srcs), "-o", str(tmp)])
-    os.replace(tmp, HOST_SO)
-    _stamp(HOST_SO, digest)
-    return HOST_SO
+    os.replace(tmp, out)
+    _stamp(out, digest)
+    return out
 
 
 def hip_flags() -> list[str]:
@@ -138,6 +150,8 @@ def main(argv=None) -> int:
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--variant", action="append", default=[],
                     help="NAME=FLAGS: also build libbdx_hip_NAME.so with extra hipcc flags")
+    ap.add_argument("--sanitize", action="store_true",
+                    help="also build libbdx_host_san.so (ASan + UBSan host library)")
     ap.add_argument("--only", default="",
                     help="comma-separated operator TU stems to keep in variant builds")
     a = ap.parse_args(argv)
@@ -147,6 +161,8 @@ def main(argv=None) -> int:
         print("built", build_hip(a.force, a.jobs, fl.split(), name, only))
     if a.variant and not (a.host or a.hip):
         return 0
+    if a.sanitize:
+        print("built", build_host(a.force, sanitize=True))
     both = not (a.host or a.hip)
     if a.host or both:
         print("built", build_host(a.force))

@@ -58,8 +58,10 @@ def host():
     global _host
     with _lock:
         if _host is None:
-            path = _build.build_host()
+            # BDX_HOST_LIB: an alternative build (the ASan/UBSan library)
+            path = os.environ.get("BDX_HOST_LIB") or _build.build_host()
             lib = ctypes.CDLL(str(path))
+            _loaded["host"] = str(path)
             for suf, ft in (("f64", f64), ("f32", f32)):
                 _declare(lib, f"bdx_cpu_stiffness_{suf}",
                          [vp, i32, vp, vp, vp, vp, vp, i32, vp, ft, vp, vp, vp, vp, vp])
@@ -126,7 +128,7 @@ def build_flags() -> dict:
 def loaded_libraries() -> list[str]:
     out = []
     if _host is not None:
-        out.append(str(_build.HOST_SO))
+        out.append(_loaded.get("host", str(_build.HOST_SO)))
     if _hip is not None:
         out.append(_loaded.get("hip", str(_build.HIP_SO)))
     return out
