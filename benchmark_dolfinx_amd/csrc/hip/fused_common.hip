@@ -277,6 +277,14 @@ BDX_CGI(float, f32)
 
 // Timing-only phase drops compiled into this TU (0 in a valid build).
 int bdx_drop_flags_common() { return BDX_UPD_DROP; }
+// Timing-only stage drops of the fused2 / fused3 cores (BDX_X_*, BDX_X3_*),
+// one bit each; nonzero = wrong numerics (bench.py refuses to time it).
+int bdx_drop_flags_f23() {
+  return (BDX_X_NOSTAGE ? 1 : 0) | (BDX_X_NOOUT ? 2 : 0) | (BDX_X_NOFRONT ? 4 : 0) |
+         (BDX_X_NOGRAD ? 8 : 0) | (BDX_X_NOTGRAD ? 16 : 0) | (BDX_X_NOBACK ? 32 : 0) |
+         (BDX_X3_NOFZ ? 64 : 0) | (BDX_X3_NOFY ? 128 : 0) | (BDX_X3_NOXF ? 256 : 0) |
+         (BDX_X3_NOBY ? 512 : 0) | (BDX_X3_NOBZ ? 1024 : 0) | (BDX_X3_NOSYNC ? 2048 : 0);
+}
 
 // Tile shape (cells in y, z) used by the fused kernel for a given nq.
 int bdx_fused_tile(int nq, int* ty, int* tz) {

@@ -44,6 +44,9 @@
 #ifndef BDX_X3_NOSYNC
 #define BDX_X3_NOSYNC 0
 #endif
+#ifndef BDX_F3_ORECOMP
+#define BDX_F3_ORECOMP 1
+#endif
 template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 2; };
 // Waves per SIMD the general (trilinear, AFF = 0) instances are compiled for:
 // at NQ = 5 the per-point geometry needs ~250 VGPRs, and forcing the default 3
@@ -212,14 +215,12 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
   }
-  // ---- per-thread output descriptors (planes 0..P of a layer)
-  int o_src[NOUT][2], o_off[NOUT], o_meta[NOUT];
-#pragma unroll
-  for (int k = 0; k < NOUT; ++k) {
-    const int e = tid + k * NT;
-    o_src[k][0] = o_src[k][1] = ZSLOT | (ZSLOT << 16);
-    o_off[k] = 0;
-    o_meta[k] = 0;
+  // ---- per-thread output descriptors (planes 0..P of a layer): slot e's
+  // <= 4 LDS sources (packed 16-bit pairs), destination offset and meta
+  auto out_desc = [&](int e, int& s0, int& s1, int& off_o, int& meta_o) {
+    s0 = s1 = ZSLOT | (ZSLOT << 16);
+    off_o = 0;
+    meta_o = 0;
     if (e < ND * PL) {
       const int pl = e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
       const int f = yz_flags(ly, lz);
@@ -234,8 +235,8 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
           for (int ccz = czl; ccz <= czh; ++ccz)
             src[ns++] = EBUF * NWBUF + (ccy * TZ + ccz) * PC + (ly - ccy * P) * P1 +
                         (lz - ccz * P) * RP + pl;
-        o_src[k][0] = src[0] | (src[1] << 16);
-        o_src[k][1] = src[2] | (src[3] << 16);
+        s0 = src[0] | (src[1] << 16);
+        s1 = src[2] | (src[3] << 16);
         const int gy = y0 + ly, gz = z0 + lz;
         const bool iy = ly < oy, iz = lz < oz;
         int kind, off;
@@ -252,10 +253,19 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
           kind = 3;
           off = static_cast<int>(pl * A.cbps) + ty * (A.ntz - 1) + tz;
         }
-        o_off[k] = off;
-        o_meta[k] = f | (kind << 4) | (pl << 8) | (rem << 12);
+        off_o = off;
+        meta_o = f | (kind << 4) | (pl << 8) | (rem << 12);
       }
     }
+  };
+  // General instances recompute them per layer in the gather (frees 4 NOUT
+  // VGPRs: the Q6 general CG instance spilled 34 dwords with them resident)
+  constexpr bool ORECOMP = BDX_F3_ORECOMP && !AFF;
+  int o_src[ORECOMP ? 1 : NOUT][2], o_off[ORECOMP ? 1 : NOUT], o_meta[ORECOMP ? 1 : NOUT];
+  if constexpr (!ORECOMP) {
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k)
+      out_desc(tid + k * NT, o_src[k][0], o_src[k][1], o_off[k], o_meta[k]);
   }
   // ---- carried-plane copy descriptors (plane P of a slab -> plane 0 of the next)
   int cp_lds[NCP];
@@ -658,11 +668,20 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
                                   A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
 #pragma unroll
       for (int k = 0; k < NOUT; ++k) {
-        const int m = o_meta[k];
+        int os0, os1, ooff, m;
+        if constexpr (ORECOMP) {
+          int e = tid + k * NT;
+          asm volatile("" : "+v"(e));  // recompute here, not hoisted out of the march
+          out_desc(e, os0, os1, ooff, m);
+        } else {
+          os0 = o_src[k][0];
+          os1 = o_src[k][1];
+          ooff = o_off[k];
+          m = o_meta[k];
+        }
         if (BDX_X_NOOUT || !(m & kValid)) continue;
         const int pl = (m >> 8) & 15, rem = m >> 12;
-        T v = s_wa[o_src[k][0] & 0xffff] + s_wa[o_src[k][0] >> 16] +
-              s_wa[o_src[k][1] & 0xffff] + s_wa[o_src[k][1] >> 16];
+        T v = s_wa[os0 & 0xffff] + s_wa[os0 >> 16] + s_wa[os1 & 0xffff] + s_wa[os1 >> 16];
         if (pl == 0) v += s_c[cur][rem];
         if (pl == P && !last) {
           s_c[nxt][rem] = v;
@@ -679,7 +698,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
           v = T(0);
         }
         T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
-        dst[o_off[k]] = v;
+        dst[ooff] = v;
       }
     }
 

@@ -107,7 +107,8 @@ def build_flags() -> dict:
     lib = hip()
     drops = {}
     for name, key in (("bdx_drop_flags_common", "BDX_UPD_DROP"),
-                      ("bdx_drop_flags_f4", "BDX_F4_DROP")):
+                      ("bdx_drop_flags_f4", "BDX_F4_DROP"),
+                      ("bdx_drop_flags_f23", "BDX_X_*/BDX_X3_*")):
         if hasattr(lib, name):
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
