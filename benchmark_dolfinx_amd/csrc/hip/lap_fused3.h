@@ -258,9 +258,11 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
       }
     }
   };
-  // General instances recompute them per layer in the gather (frees 4 NOUT
-  // VGPRs: the Q6 general CG instance spilled 34 dwords with them resident)
-  constexpr bool ORECOMP = BDX_F3_ORECOMP && !AFF;
+  // General instances at NQ >= 7 recompute them per layer in the gather
+  // (frees 4 NOUT VGPRs: the Q6 general CG instance spilled 34 dwords with them
+  // resident; same-box Q6 general 18.8 -> 22.0 GDoF/s, while Q3 general, which
+  // did not spill, drops 18.2 -> 14.0 with the recomputation)
+  constexpr bool ORECOMP = BDX_F3_ORECOMP && !AFF && NQ >= 7;
   int o_src[ORECOMP ? 1 : NOUT][2], o_off[ORECOMP ? 1 : NOUT], o_meta[ORECOMP ? 1 : NOUT];
   if constexpr (!ORECOMP) {
 #pragma unroll

@@ -42,9 +42,11 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         if geometry == "stored":
             kernel = "fused" if pb.kc is None else "v1"
         elif geometry == "otf-general" or not pb.all_affine:
-            # general (trilinear) cells, same-box A/B (scripts/job_r2i.sh):
-            # Q3 fused3 18.2 vs fused2 16.5 GDoF/s; Q6 18.8 both
-            kernel = "fused3" if pb.degree == 3 else "fused2"
+            # general (trilinear) cells, same-box A/B (scripts/job_r2i.sh,
+            # job_r2r.sh): Q3 fused3 18.2 vs fused2 16.5 GDoF/s; Q6 fused3
+            # 22.0 (spill-free) vs fused2 18.8; fused3 falls back to fused2
+            # where it does not apply (phi0 = I)
+            kernel = "fused3"
         else:
             # Kronecker cores on parallelepiped meshes (profiles/r1_kernel_ab.md):
             # fused4 (MFMA) for Q3 FP64 (7.8 ms/iteration vs fused5 8.1, fused3
