@@ -152,7 +152,8 @@ def run(comm, a) -> dict | None:
     value = pb.ndofs_global * a.steps / (1e9 * dt)
     ynorm = pb.norm(x)
     rt = getattr(op, "_rt", None)
-    runtime = (f"native C++ ({rt.transport}, hipGraph={rt.graphs}, overlap={rt.overlap})"
+    runtime = (f"native C++ ({rt.transport}, hipGraph={rt.graphs}, overlap={rt.overlap}, "
+               f"tiled={rt.tiled})"
                if rt is not None else "python")
     comm_info = {"torch_backend": comm.backend, "torch_world": comm.size,
                  "transport": rt.transport if rt is not None else "python",

@@ -121,9 +121,20 @@ constexpr int kBoxFields = 7;
 // pass to one box: the owned lower-face boxes overlap on edges/corners (a dof
 // there receives partial sums from up to 7 neighbours), so the add-unpack runs
 // box by box -- race-free and in a fixed order.
+// Storage index of lattice node (i, j, k): the lattice layout or the tiled
+// one of the CG runtime (bdx_lattice.h, tsy != 0).
+struct VecIdx {
+  int64_t L1, ld, tsy, tsz, tntz, tcol;
+  __device__ __forceinline__ int64_t operator()(int64_t i, int64_t j, int64_t k) const {
+    if (tsy) return ((j / tsy) * tntz + k / tsz) * tcol + (i * tsy + j % tsy) * tsz + k % tsz;
+    return (i * L1 + j) * ld + k;
+  }
+};
+
+// Pack / unpack of the halo boxes (see the box table above).
 template <typename T, int MODE>
 __global__ void __launch_bounds__(kBlock)
-    box_copy_kernel(T* __restrict__ vec, int64_t L1, int64_t ld,
+    box_copy_kernel(T* __restrict__ vec, VecIdx vi,
                     const int64_t* __restrict__ boxes, int nboxes, int64_t total,
                     T* __restrict__ buf, int only = -1) {
   int64_t t0 = 0, t1 = total;
@@ -139,7 +150,7 @@ __global__ void __launch_bounds__(kBlock)
     const int64_t o = t - bx[6];
     const int64_t e1 = bx[4], e2 = bx[5];
     const int64_t k = o % e2, j = (o / e2) % e1, i = o / (e1 * e2);
-    const int64_t v = ((bx[0] + i) * L1 + (bx[1] + j)) * ld + (bx[2] + k);
+    const int64_t v = vi(bx[0] + i, bx[1] + j, bx[2] + k);
     if constexpr (MODE == 0)
       buf[t] = vec[v];
     else if constexpr (MODE == 1)
@@ -147,6 +158,43 @@ __global__ void __launch_bounds__(kBlock)
     else
       vec[v] += buf[t];
   }
+}
+
+// Lattice layout <-> tiled layout of one vector, every node of the local
+// lattice (owned and ghost).  dir 0: tiled[t(i,j,k)] = lat[l(i,j,k)]; 1: back.
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+    layout_convert_kernel(int dir, VecIdx lat, VecIdx til, int64_t L0, int64_t L1v,
+                          int64_t L2, T* __restrict__ a, T* __restrict__ t) {
+  const int64_t n = L0 * L1v * L2;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n;
+       e += static_cast<int64_t>(gridDim.x) * kBlock) {
+    // e enumerates the tiled order (tile, x, ly, lz) of valid nodes would need
+    // divisions by run-time tile sizes; enumerate lattice order instead (the
+    // lattice side then streams, the tiled side moves in 8..16-node runs)
+    const int64_t k = e % L2, r = e / L2, j = r % L1v, i = r / L1v;
+    if (dir == 0)
+      t[til(i, j, k)] = a[lat(i, j, k)];
+    else
+      a[lat(i, j, k)] = t[til(i, j, k)];
+  }
+}
+
+template <typename T>
+int box_copy_vi(int mode, T* vec, VecIdx vi, const int64_t* boxes, int nboxes, int64_t total,
+                T* buf, hipStream_t st) {
+  if (total <= 0) return 0;
+  const int64_t g64 = (total + kBlock - 1) / kBlock;
+  const int g = static_cast<int>(g64 < 4096 ? g64 : 4096);
+  if (mode == 0) {
+    box_copy_kernel<T, 0><<<g, kBlock, 0, st>>>(vec, vi, boxes, nboxes, total, buf);
+  } else if (mode == 1) {
+    box_copy_kernel<T, 1><<<g, kBlock, 0, st>>>(vec, vi, boxes, nboxes, total, buf);
+  } else {  // add: boxes may overlap (edges/corners), one launch per box
+    for (int b = 0; b < nboxes; ++b)
+      box_copy_kernel<T, 2><<<g, kBlock, 0, st>>>(vec, vi, boxes, nboxes, total, buf, b);
+  }
+  return static_cast<int>(hipGetLastError());
 }
 
 int grid_for_rows(int64_t nrows) {
@@ -208,19 +256,29 @@ int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
   int bdx_box_copy_##SUF(int mode, T* vec, int64_t L1, int64_t ld,            \
                          const int64_t* boxes, int nboxes, int64_t total,     \
                          T* buf, hipStream_t st) {                            \
-    if (total <= 0) return 0;                                                 \
-    int64_t g64 = (total + kBlock - 1) / kBlock;                              \
-    const int g = static_cast<int>(g64 < 4096 ? g64 : 4096);                  \
-    if (mode == 0)                                                            \
-      box_copy_kernel<T, 0><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
-                                                  total, buf);                \
-    else if (mode == 1)                                                       \
-      box_copy_kernel<T, 1><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
-                                                  total, buf);                \
-    else /* add: boxes may overlap (edges/corners), one launch per box */     \
-      for (int b = 0; b < nboxes; ++b)                                        \
-        box_copy_kernel<T, 2><<<g, kBlock, 0, st>>>(vec, L1, ld, boxes, nboxes, \
-                                                    total, buf, b);           \
+    const VecIdx vi{L1, ld, 0, 0, 0, 0};                                      \
+    return box_copy_vi<T>(mode, vec, vi, boxes, nboxes, total, buf, st);      \
+  }                                                                           \
+  /* the same on a lattice descriptor (lattice or tiled storage) */           \
+  int bdx_box_copy_lat_##SUF(int mode, T* vec, const int64_t* latd,           \
+                             const int64_t* boxes, int nboxes, int64_t total, \
+                             T* buf, hipStream_t st) {                        \
+    const BdxLattice L = BdxLattice::from(latd);                              \
+    const VecIdx vi{L.L[1], L.ld, L.tsy, L.tsz, L.tntz, L.tcol};              \
+    return box_copy_vi<T>(mode, vec, vi, boxes, nboxes, total, buf, st);      \
+  }                                                                           \
+  /* lattice <-> tiled copy of a vector (dir 0: to tiled, 1: back) */         \
+  int bdx_layout_convert_##SUF(int dir, const int64_t* latd_tiled, T* lat,    \
+                               T* tiled, hipStream_t st) {                    \
+    const BdxLattice L = BdxLattice::from(latd_tiled);                        \
+    if (!L.tsy) return static_cast<int>(hipErrorInvalidValue);                \
+    const VecIdx lv{L.L[1], L.ld, 0, 0, 0, 0};                                \
+    const VecIdx tv{L.L[1], L.ld, L.tsy, L.tsz, L.tntz, L.tcol};              \
+    const int64_t n = L.L[0] * L.L[1] * L.L[2];                               \
+    const int64_t g64 = (n + kBlock - 1) / kBlock;                            \
+    const int g = static_cast<int>(g64 < 65536 ? g64 : 65536);                \
+    layout_convert_kernel<T><<<g, kBlock, 0, st>>>(dir, lv, tv, L.L[0], L.L[1], \
+                                                   L.L[2], lat, tiled);       \
     return static_cast<int>(hipGetLastError());                               \
   }
 

@@ -187,6 +187,87 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
+// The r update of the tiled storage (bdx_lattice.h, tsy != 0): the same
+// arithmetic per node as the flat kernel above, in the layout's element order.
+// Chunks of tsy * tsz elements are one tile's patch of one x-plane; a vector
+// of W elements never straddles a chunk (tsy * tsz * sizeof(T) is a multiple
+// of 16 bytes, checked by the host wrapper).
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cg_update_tiled_kernel(int64_t L0, int64_t L1, int64_t Lz, int tsy, int tsz, int tntz,
+                           int64_t o0, int64_t o1, int64_t o2, int64_t nvec, T* __restrict__ r,
+                           const T* __restrict__ y, const T* __restrict__ yb,
+                           const T* __restrict__ zb, const T* __restrict__ cb, int nty, int ntz,
+                           const double* __restrict__ scal, int rn_slot, int pap_slot,
+                           double* __restrict__ partials) {
+  __shared__ double lds[16];
+  const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
+  constexpr int W = 16 / sizeof(T);
+  typedef T V __attribute__((ext_vector_type(W)));
+  const int64_t ch = static_cast<int64_t>(tsy) * tsz;
+  const double inv_ch = 1.0 / static_cast<double>(ch), inv_l0 = 1.0 / static_cast<double>(L0);
+  const float inv_tsz = 1.0f / static_cast<float>(tsz);
+  double acc = 0.0;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t e0 = v * W;
+    int64_t c = static_cast<int64_t>(static_cast<double>(e0) * inv_ch);  // chunk
+    if (c * ch > e0) --c;
+    if ((c + 1) * ch <= e0) ++c;
+    int64_t blk = static_cast<int64_t>(static_cast<double>(c) * inv_l0);
+    if (blk * L0 > c) --blk;
+    if ((blk + 1) * L0 <= c) ++blk;
+    const int64_t x = c - blk * L0;
+    const int tY = static_cast<int>(blk / tntz), tZ = static_cast<int>(blk - static_cast<int64_t>(tY) * tntz);
+    if (x >= o0) continue;
+    const int ein = static_cast<int>(e0 - c * ch);
+    const V vy = *reinterpret_cast<const V*>(y + e0);
+    V vr = *reinterpret_cast<const V*>(r + e0);
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int e = ein + w;
+      int ly = static_cast<int>(static_cast<float>(e) * inv_tsz);
+      if (ly * tsz > e) --ly;
+      if ((ly + 1) * tsz <= e) ++ly;
+      const int lz = e - ly * tsz;
+      const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz = static_cast<int64_t>(tZ) * tsz + lz;
+      if (gy >= o1 || gz >= o2) continue;
+      any = true;
+      const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
+      T t = vy[w];
+      if (yrow >= 0) t += yb[(x * (nty - 1) + yrow) * Lz + gz];
+      if (lz == 0 && tZ >= 1 && tZ < ntz) {
+        t += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
+        if (yrow >= 0) t += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
+      }
+      const T rn = vr[w] - alpha * t;
+      vr[w] = rn;
+      acc += static_cast<double>(rn) * static_cast<double>(rn);
+    }
+    if (any) *reinterpret_cast<V*>(r + e0) = vr;
+  }
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+// x += (s[num] / s[den]) p over a whole flat vector (the tiled storage: its
+// padding is zero in p, so it stays zero in x).
+template <typename T>
+__global__ void __launch_bounds__(256)
+    xflush_flat_kernel(int64_t nvec, T* __restrict__ x, const T* __restrict__ p,
+                       const double* __restrict__ scal, int num, int den) {
+  const T alpha = static_cast<T>(scal[num] / scal[den]);
+  constexpr int W = 16 / sizeof(T);
+  typedef T V __attribute__((ext_vector_type(W)));
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * 256) {
+    V xv = reinterpret_cast<V*>(x)[v];
+    xv += alpha * reinterpret_cast<const V*>(p)[v];
+    reinterpret_cast<V*>(x)[v] = xv;
+  }
+}
+
 // x += (s[num] / s[den]) p over the owned rows (flush of the lagged x update).
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -274,6 +355,45 @@ extern "C" {
 BDX_CGI(double, f64)
 BDX_CGI(float, f32)
 #undef BDX_CGI
+
+// Tiled-storage variants of the r update and the x flush (latd: the tiled
+// descriptor of bdx_lattice.h).
+#define BDX_CGT(T, SUF)                                                                         \
+  int bdx_cg_update_tiled_##SUF(const int64_t* latd, const int64_t* own, T* r, const T* y,     \
+                                const T* yb, const T* zb, const T* cb, int nty, int ntz,       \
+                                double* scal, int rn_slot, int pap_slot, int out_slot,         \
+                                double* partials, hipStream_t st) {                            \
+    const BdxLattice L = BdxLattice::from(latd);                                               \
+    if (!L.tsy || (L.tsy * L.tsz * static_cast<int64_t>(sizeof(T))) % 16)                     \
+      return static_cast<int>(hipErrorInvalidValue);                                           \
+    const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
+    const int64_t want = (nvec + 255) / 256;                                                   \
+    const int g = static_cast<int>(want < BDX_UPD_GRID ? (want > 0 ? want : 1) : BDX_UPD_GRID); \
+    cg_update_tiled_kernel<T><<<g, 256, 0, st>>>(                                              \
+        L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),              \
+        static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,    \
+        scal, rn_slot, pap_slot, partials);                                                    \
+    if (g > 4 * kStage1) {                                                                     \
+      double* stage = partials + kPartialsCap - kStage1;                                       \
+      reduce_partials_slices<<<kStage1, 256, 0, st>>>(partials, g, stage);                     \
+      reduce_partials_fixed<<<1, 256, 0, st>>>(stage, kStage1, scal, out_slot);                \
+    } else {                                                                                   \
+      reduce_partials_fixed<<<1, 256, 0, st>>>(partials, g, scal, out_slot);                   \
+    }                                                                                          \
+    return static_cast<int>(hipGetLastError());                                                \
+  }                                                                                            \
+  int bdx_xflush_tiled_##SUF(const int64_t* latd, T* x, const T* p, const double* scal, int num, \
+                             int den, hipStream_t st) {                                        \
+    const BdxLattice L = BdxLattice::from(latd);                                               \
+    const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
+    const int64_t want = (nvec + 255) / 256;                                                   \
+    const int g = static_cast<int>(want < 65536 ? (want > 0 ? want : 1) : 65536);              \
+    xflush_flat_kernel<T><<<g, 256, 0, st>>>(nvec, x, p, scal, num, den);                      \
+    return static_cast<int>(hipGetLastError());                                                \
+  }
+BDX_CGT(double, f64)
+BDX_CGT(float, f32)
+#undef BDX_CGT
 
 // Timing-only phase drops compiled into this TU (0 in a valid build).
 int bdx_drop_flags_common() { return BDX_UPD_DROP; }

@@ -725,7 +725,7 @@ __global__ void __launch_bounds__(256)
         add += zb[(x * Ly + yy) * (ntz - 1) + (tzz - 1)];
         add += cb[(x * (nty - 1) + tym1) * (ntz - 1) + (tzz - 1)];
       }
-      y[lat.idx(x, yy, z)] += add;
+      y[lat.sidx(x, yy, z)] += add;
     } else {
       const int64_t s = t - n1;
       const int64_t tzm1 = s % (ntz - 1);
@@ -735,7 +735,7 @@ __global__ void __launch_bounds__(256)
       if (yy % sy == 0 && tyy >= 1 && tyy < nty) continue;  // handled by the YB pass
       const int64_t z = (tzm1 + 1) * sz;
       if (ghost_only && lat.is_owned(x, yy, z)) continue;
-      y[lat.idx(x, yy, z)] += zb[s];
+      y[lat.sidx(x, yy, z)] += zb[s];
     }
   }
 }
@@ -771,21 +771,21 @@ __global__ void __launch_bounds__(256)
         add += zb[(x * Ly + yy) * (ntz - 1) + (tzz - 1)];
         add += cb[(x * (nty - 1) + tym1) * (ntz - 1) + (tzz - 1)];
       }
-      y[lat.idx(x, yy, z)] += add;
+      y[lat.sidx(x, yy, z)] += add;
     } else if (t < nA1 + nA2) {  // ZB column entry on the x ghost plane
       const int64_t s = t - nA1, x = Lx - 1;
       const int64_t tzm1 = s % (ntz - 1), yy = s / (ntz - 1);
       const int64_t tyy = yy / sy;
       if (yy % sy == 0 && tyy >= 1 && tyy < nty) continue;  // on a YB row: done above
-      y[lat.idx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
+      y[lat.sidx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
     } else if (t < nA1 + nA2 + nB) {  // ZB column entry on the y ghost plane
       const int64_t s = t - nA1 - nA2, yy = Ly - 1;
       const int64_t tzm1 = s % (ntz - 1), x = s / (ntz - 1);
-      y[lat.idx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
+      y[lat.sidx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
     } else {  // YB row entry on the z ghost plane
       const int64_t s = t - nA1 - nA2 - nB, z = Lz - 1;
       const int64_t tym1 = s % (nty - 1), x = s / (nty - 1);
-      y[lat.idx(x, (tym1 + 1) * sy, z)] += yb[(x * (nty - 1) + tym1) * Lz + z];
+      y[lat.sidx(x, (tym1 + 1) * sy, z)] += yb[(x * (nty - 1) + tym1) * Lz + z];
     }
   }
 }

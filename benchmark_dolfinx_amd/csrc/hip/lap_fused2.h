@@ -78,7 +78,21 @@ struct Fused2Args {
   int beta_num, beta_den;        // CG: beta = scal[num] / scal[den]; num < 0 -> 0
   int xa_num, xa_den;            // CG: alpha_prev = scal[num] / scal[den]; num < 0 -> no x update
   T kappa;
+  // tiled vector storage (bdx_lattice.h; tsy = 0: lattice layout): the
+  // x-plane stride ps is then tsy * tsz and a node's (y, z) offset is its
+  // tile's column base plus the in-tile position (fused4 / fused5 only)
+  int tsy, tsz, tntz;
+  int64_t tcol;
 };
+
+// (y, z) part of a vector offset (the x-plane part is x * ps)
+template <typename T>
+__host__ __device__ __forceinline__ int64_t fused_yzoff(const Fused2Args<T>& A, int gy, int gz) {
+  if (A.tsy)
+    return (static_cast<int64_t>(gy / A.tsy) * A.tntz + gz / A.tsz) * A.tcol +
+           (gy % A.tsy) * A.tsz + gz % A.tsz;
+  return static_cast<int64_t>(gy) * A.ld + gz;
+}
 
 // fused2: x-march over (y, z) tiles with general (trilinear) or affine geometry.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
@@ -763,6 +777,15 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
   // 32-bit per-layer offsets: one layer of the vector must be < 2^31 elements
   if ((P + 1) * L.L[1] * L.ld >= (int64_t(1) << 31)) return static_cast<int>(hipErrorInvalidValue);
   a.ps = L.L[1] * L.ld;
+  a.tsy = static_cast<int>(L.tsy);
+  a.tsz = static_cast<int>(L.tsz);
+  a.tntz = static_cast<int>(L.tntz);
+  a.tcol = L.tcol;
+  if (L.tsy) {
+    // tiled: in-tile offsets are whole-vector offsets, still 32-bit
+    if (L.size() >= (int64_t(1) << 31) || L.tsz <= 0) return static_cast<int>(hipErrorInvalidValue);
+    a.ps = L.tsy * L.tsz;
+  }
   a.ybps = static_cast<int64_t>(nty - 1) * L.L[2];
   a.zbps = L.L[1] * static_cast<int64_t>(ntz - 1);
   a.cbps = static_cast<int64_t>(nty - 1) * (ntz - 1);
@@ -870,6 +893,7 @@ inline int fused_set_segments(Fused2Args<T>& a, int nseg) {
       int nty, int ntz, const int* rect, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
+    if (a.tsy) return static_cast<int>(hipErrorInvalidValue); /* lattice layout only */ \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
     BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
     mode &= 0xff;                                                                  \

@@ -808,6 +808,7 @@ int fused3_resident(int affine) {
       int nty, int ntz, const int* rect, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
+    if (a.tsy) return static_cast<int>(hipErrorInvalidValue); /* lattice layout only */ \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
     BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
     mode &= 0xff;                                                                  \

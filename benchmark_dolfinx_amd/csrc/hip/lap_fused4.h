@@ -39,7 +39,7 @@
 #endif
 // Timing-only phase drops for A/B attribution (wrong numerics when nonzero):
 // 1 = MFMA core, 2 = gather + write-out, 4 = next-layer global loads,
-// 8 = x contraction + geometry.
+// 8 = x contraction + geometry, 16 = the two workgroup barriers per layer.
 #ifndef BDX_F4_RP
 #define BDX_F4_RP 4
 #endif
@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       const int f = yz_flags(ly, lz);
       // invalid (off-lattice) slots keep offset 0: the prefetch loads them
       // unconditionally (in bounds, value unused)
-      if (f & kValid) st_goff[k] = (pl * Ly + y0 + ly) * ld + z0 + lz;
+      if (f & kValid) st_goff[k] = static_cast<int>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz));
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
   }
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         int kind, off;
         if (iy && iz) {
           kind = 0;
-          off = (pl * Ly + gy) * ld + gz;
+          off = static_cast<int>(pl * A.ps + fused_yzoff(A, gy, gz));
         } else if (!iy && iz) {
           kind = 1;
           off = static_cast<int>(pl * A.ybps) + ty * Lz + gz;
@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       T v = T(0);
       if (f & kValid)
         v = stage(f, cbeg * P + pl, A.u + l0, A.pnew + l0, A.y + l0,
-                  (pl * Ly + y0 + ly) * ld + z0 + lz, wr);
+                  static_cast<int>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz)), wr);
       s_u[0][pl * PLP + ly * DZP + lz] = v;
     }
   }
@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     const bool last = (cx == cend - 1);   // end of this segment
     const bool glast = (cx == ncx - 1);   // end of the march
     const bool red = (cx < sa);           // redundant layer: carry only
-    __syncthreads();
+    if constexpr ((BDX_F4_DROP & 16) == 0) __syncthreads();
 
     // ---- prefetch: DEPTH 1 loads layer cx+1 into pfc (used at the end of
     // this layer); DEPTH 2 loads layer cx+2 into pfn while pfc (layer cx+1,
@@ -537,7 +537,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
 #pragma unroll
       for (int r = 0; r < ND; ++r) eo[r * P1] = cell_on ? ye[r] : T(0);
     }
-    __syncthreads();
+    if constexpr ((BDX_F4_DROP & 16) == 0) __syncthreads();
 
     // ------------------------------------------------ stage the next layer (LDS)
     // The prefetched values go to LDS before any global store of this layer

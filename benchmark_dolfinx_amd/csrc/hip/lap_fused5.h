@@ -248,7 +248,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     if (e < P * PL) {
       const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
       const int f = yz_flags(ly, lz);
-      st_goff[k] = static_cast<unsigned>((pl * Ly + y0 + ly) * ld + z0 + lz);
+      st_goff[k] = static_cast<unsigned>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz));
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
   }
@@ -281,7 +281,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
         int kind, off;
         if (iy && iz) {
           kind = 0;
-          off = (pl * Ly + gy) * ld + gz;
+          off = static_cast<int>(pl * A.ps + fused_yzoff(A, gy, gz));
         } else if (!iy && iz) {
           kind = 1;
           off = static_cast<int>(pl * A.ybps) + ty * Lz + gz;
@@ -326,7 +326,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       T v = T(0);
       if (f & kValid)
         v = stage(f, cbeg * P + pl, A.u + l0, A.pnew + l0, A.y + l0,
-                  (pl * Ly + y0 + ly) * ld + z0 + lz, wr);
+                  static_cast<int>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz)), wr);
       s_u[0][pl * PLP + ly * DZP + lz] = v;
     }
   }

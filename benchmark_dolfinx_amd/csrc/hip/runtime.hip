@@ -72,6 +72,22 @@ int bdx_xflush_f64(const int64_t*, const int64_t*, double*, const double*, const
                    int, hipStream_t);
 int bdx_xflush_f32(const int64_t*, const int64_t*, float*, const float*, const double*, int,
                    int, hipStream_t);
+int bdx_box_copy_lat_f64(int, double*, const int64_t*, const int64_t*, int, int64_t, double*,
+                         hipStream_t);
+int bdx_box_copy_lat_f32(int, float*, const int64_t*, const int64_t*, int, int64_t, float*,
+                         hipStream_t);
+int bdx_layout_convert_f64(int, const int64_t*, double*, double*, hipStream_t);
+int bdx_layout_convert_f32(int, const int64_t*, float*, float*, hipStream_t);
+int bdx_cg_update_tiled_f64(const int64_t*, const int64_t*, double*, const double*, const double*,
+                            const double*, const double*, int, int, double*, int, int, int,
+                            double*, hipStream_t);
+int bdx_cg_update_tiled_f32(const int64_t*, const int64_t*, float*, const float*, const float*,
+                            const float*, const float*, int, int, double*, int, int, int, double*,
+                            hipStream_t);
+int bdx_xflush_tiled_f64(const int64_t*, double*, const double*, const double*, int, int,
+                         hipStream_t);
+int bdx_xflush_tiled_f32(const int64_t*, float*, const float*, const double*, int, int,
+                         hipStream_t);
 }
 
 // The fused2..5 operator entry points (lap_fused{2,3,4,5}_<suf>_p<P>.hip);
@@ -356,7 +372,8 @@ enum Mark {
 };
 
 struct RtConfig {
-  int64_t latd[17];
+  int64_t latd[21];
+  int64_t latdT[21];  // tiled-storage descriptor (tsy = 0: lattice layout)
   int64_t own[3];
   int version, affine, P, nq, nblocks, nty, ntz, sy, sz, nseg;
   double kappa;
@@ -378,6 +395,14 @@ struct CGRuntime {
   std::vector<T> tabs_host;
   const T* tabs = nullptr;  // host copy (fused2-4: kernarg tables) or device buffer (fused5)
   T *x, *r, *pa, *pb, *y, *yb, *zb, *cb;
+  // Tiled storage (cfg.latdT[17] != 0): the iteration runs on tiled copies
+  // xt, rt, pat, pbt, yt (allocated zeroed by the caller: the padding stays
+  // zero); r and x are imported after each prologue and x is exported after
+  // every iterate() / profile().  wx .. wy: the buffers the loop works on.
+  bool tiled = false, need_import = false;
+  T *xt = nullptr, *rt_ = nullptr, *pat = nullptr, *pbt = nullptr, *yt = nullptr;
+  T *wx, *wr, *wpa, *wpb, *wy;
+  const int64_t* wlatd = nullptr;
   const T* xv;
   const T* kc = nullptr;
   double *scal, *partials, *upart;
@@ -405,12 +430,27 @@ struct CGRuntime {
   }
   int box_copy(int mode, T* vec, const int64_t* boxes, int nb, int64_t total, T* buf,
                hipStream_t s) {
-    const BdxLattice L = BdxLattice::from(cfg.latd);
     if constexpr (sizeof(T) == 8)
-      return bdx_box_copy_f64(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, s);
+      return bdx_box_copy_lat_f64(mode, vec, wlatd, boxes, nb, total, buf, s);
     else
-      return bdx_box_copy_f32(mode, vec, L.L[1], L.ld, boxes, nb, total, buf, s);
+      return bdx_box_copy_lat_f32(mode, vec, wlatd, boxes, nb, total, buf, s);
   }
+  int convert(int dir, T* lat, T* til, hipStream_t s) {
+    if constexpr (sizeof(T) == 8)
+      return bdx_layout_convert_f64(dir, cfg.latdT, lat, til, s);
+    else
+      return bdx_layout_convert_f32(dir, cfg.latdT, lat, til, s);
+  }
+  // tiled: bring the prologue's r and x into the tiled copies, p_old = 0
+  int import_state() {
+    if (!tiled || !need_import) return 0;
+    need_import = false;
+    int rc;
+    if ((rc = convert(0, r, rt_, st)) || (rc = convert(0, x, xt, st))) return rc;
+    const BdxLattice L = BdxLattice::from(cfg.latdT);
+    return static_cast<int>(hipMemsetAsync(pat, 0, L.size() * sizeof(T), st));
+  }
+  int export_x() { return tiled ? convert(1, x, xt, st) : 0; }
   // forward: owned lower faces of v -> peers' ghost planes (pack, exchange, unpack)
   int halo_forward(T* v, hipStream_t s) {
     int rc = box_copy(0, v, face_boxes, nface_boxes, face_total, hbuf_a, s);
@@ -431,20 +471,23 @@ struct CGRuntime {
   }
   int finalize_ghost(hipStream_t s) {
     if constexpr (sizeof(T) == 8)
-      return bdx_fused_finalize_f64(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
+      return bdx_fused_finalize_f64(wlatd, wy, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
                                     s);
     else
-      return bdx_fused_finalize_f32(cfg.latd, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
+      return bdx_fused_finalize_f32(wlatd, wy, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
                                     s);
   }
 
   // One CG iteration with explicit parity / flags (stream-ordered, no sync).
   int step(long k, bool first, bool xlag) {
     const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
-    T* pold = (k % 2 == 0) ? pa : pb;
-    T* pnew = (k % 2 == 0) ? pb : pa;
+    T* pold = (k % 2 == 0) ? wpa : wpb;
+    T* pnew = (k % 2 == 0) ? wpb : wpa;
+    T* const r = wr;
+    T* const x = wx;
+    T* const y = wy;
     auto op = [&](const int* rect, hipStream_t s) {
-      return apply(1 | (cfg.nseg << 8), cfg.affine, cfg.latd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
+      return apply(1 | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
                    pnew, x, y, yb, zb, cb, xv, kc, tabs, cfg.kappa, scal, partials,
                    first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1,
                    cfg.nty, cfg.ntz, rect, s);
@@ -490,12 +533,20 @@ struct CGRuntime {
     if ((rc = bdx_reduce_partials(partials, cfg.nblocks, scal, kPAP, st))) return rc;
     if (nranks > 1 && (rc = tr->allreduce_sum(scal + kPAP, 1, st))) return rc;
     mark(kMPap, st);
-    if constexpr (sizeof(T) == 8)
+    if (tiled) {
+      if constexpr (sizeof(T) == 8)
+        rc = bdx_cg_update_tiled_f64(wlatd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, scal, cur,
+                                     kPAP, nxt, upart, st);
+      else
+        rc = bdx_cg_update_tiled_f32(wlatd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, scal, cur,
+                                     kPAP, nxt, upart, st);
+    } else if constexpr (sizeof(T) == 8) {
       rc = bdx_cg_update_iface_f64(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
                                    cfg.sz, scal, cur, kPAP, nxt, upart, st);
-    else
+    } else {
       rc = bdx_cg_update_iface_f32(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
                                    cfg.sz, scal, cur, kPAP, nxt, upart, st);
+    }
     if (rc) return rc;
     mark(kMUpd, st);
     if (nranks > 1 && (rc = tr->allreduce_sum(scal + nxt, 1, st))) return rc;
@@ -542,6 +593,7 @@ struct CGRuntime {
   }
 
   int iterate_on_stream(long n) {
+    if (int rc = import_state()) return rc;
     for (long i = 0; i < n; ++i) {
       const bool first = (it == 0);
       const int par = static_cast<int>(it % 2);
@@ -565,8 +617,16 @@ struct CGRuntime {
   int flush() {
     if (!x_lag) return 0;
     const int last = ((it - 1) % 2 == 0) ? kRR0 : kRR1;
-    T* plast = ((it - 1) % 2 == 0) ? pb : pa;  // p_new of the last iteration
+    T* plast = ((it - 1) % 2 == 0) ? wpb : wpa;  // p_new of the last iteration
     x_lag = false;
+    int rc;
+    if (tiled) {
+      if constexpr (sizeof(T) == 8)
+        rc = bdx_xflush_tiled_f64(wlatd, wx, plast, scal, last, kPAP, st);
+      else
+        rc = bdx_xflush_tiled_f32(wlatd, wx, plast, scal, last, kPAP, st);
+      return rc ? rc : export_x();
+    }
     if constexpr (sizeof(T) == 8)
       return bdx_xflush_f64(cfg.latd, cfg.own, x, plast, scal, last, kPAP, st);
     else
@@ -583,7 +643,7 @@ struct CGRuntime {
     BDX_CHECK(hipEventRecord(ev_in, ext));
     BDX_CHECK(hipStreamWaitEvent(st, ev_in, 0));
     prof = true;
-    int rc = 0;
+    int rc = import_state();
     for (long i = 0; i < n && !rc; ++i) {
       const bool first = (it == 0);
       rc = step(it, first, x_lag);
@@ -636,10 +696,13 @@ template <typename T>
 Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, double kappa,
                const double* wts, const double* qpts, const void* tabs, void* const* ptrs,
                const int64_t* halo_sizes, const int64_t* face_cnt, const int64_t* ghost_cnt,
-               int transport, int nranks, int rank, int64_t group_id, hipStream_t st) {
+               int transport, int nranks, int rank, int64_t group_id, hipStream_t st,
+               const int64_t* latd_tiled, void* const* tptrs) {
   auto rt = std::make_unique<CGRuntime<T>>();
   RtConfig& c = rt->cfg;
   std::memcpy(c.latd, latd, sizeof(c.latd));
+  std::memset(c.latdT, 0, sizeof(c.latdT));
+  if (latd_tiled && latd_tiled[17] && tptrs) std::memcpy(c.latdT, latd_tiled, sizeof(c.latdT));
   std::memcpy(c.own, own, sizeof(c.own));
   // iparams: version, affine, P, nq, nblocks, nty, ntz, sy, sz, use_graph, overlap, nseg
   // (nblocks = nty * ntz * nseg p.Ap partials)
@@ -685,6 +748,24 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   rt->face_boxes = static_cast<const int64_t*>(ptrs[i++]);
   rt->ghost_boxes = static_cast<const int64_t*>(ptrs[i++]);
   rt->kc = static_cast<const T*>(ptrs[i++]);
+  rt->tiled = c.latdT[17] != 0;
+  if (rt->tiled) {
+    // only the x-march kernels whose tile is the storage tile address it
+    if ((c.version != 4 && c.version != 5) || c.latdT[17] != c.sy || c.latdT[18] != c.sz)
+      return nullptr;
+    rt->xt = static_cast<T*>(tptrs[0]);
+    rt->rt_ = static_cast<T*>(tptrs[1]);
+    rt->pat = static_cast<T*>(tptrs[2]);
+    rt->pbt = static_cast<T*>(tptrs[3]);
+    rt->yt = static_cast<T*>(tptrs[4]);
+    if (!rt->xt || !rt->rt_ || !rt->pat || !rt->pbt || !rt->yt) return nullptr;
+  }
+  rt->wx = rt->tiled ? rt->xt : rt->x;
+  rt->wr = rt->tiled ? rt->rt_ : rt->r;
+  rt->wpa = rt->tiled ? rt->pat : rt->pa;
+  rt->wpb = rt->tiled ? rt->pbt : rt->pb;
+  rt->wy = rt->tiled ? rt->yt : rt->y;
+  rt->wlatd = rt->tiled ? c.latdT : c.latd;
   rt->nface_boxes = static_cast<int>(halo_sizes[0]);
   rt->face_total = halo_sizes[1];
   rt->nghost_boxes = static_cast<int>(halo_sizes[2]);
@@ -809,16 +890,25 @@ int bdx_rt_rccl_selftest(double* buf, int n, hipStream_t st) {
   return rc;
 }
 
+// latd_tiled / tptrs (may be null): the tiled-storage descriptor and the
+// runtime's tiled x, r, p_a, p_b, y buffers (zero-initialised by the caller).
 void* bdx_rt_create(int is_f64, const int64_t* latd, const int64_t* own, const int* iparams,
                     double kappa, const double* wts, const double* qpts, const void* tabs,
                     void* const* ptrs, const int64_t* halo_sizes, const int64_t* face_cnt,
                     const int64_t* ghost_cnt, int transport, int nranks, int rank,
-                    int64_t group_id, hipStream_t st) {
+                    int64_t group_id, hipStream_t st, const int64_t* latd_tiled,
+                    void* const* tptrs) {
   if (is_f64)
     return create<double>(latd, own, iparams, kappa, wts, qpts, tabs, ptrs, halo_sizes,
-                          face_cnt, ghost_cnt, transport, nranks, rank, group_id, st);
+                          face_cnt, ghost_cnt, transport, nranks, rank, group_id, st, latd_tiled,
+                          tptrs);
   return create<float>(latd, own, iparams, kappa, wts, qpts, tabs, ptrs, halo_sizes, face_cnt,
-                       ghost_cnt, transport, nranks, rank, group_id, st);
+                       ghost_cnt, transport, nranks, rank, group_id, st, latd_tiled, tptrs);
+}
+
+// 1 if the loop runs on the tiled storage layout.
+int bdx_rt_tiled(void* h) {
+  return with_rt(h, [](auto* rt) { return rt->tiled ? 1 : 0; });
 }
 
 // Open the runtime's RCCL communicator (collective over the ranks; every
@@ -849,6 +939,7 @@ int bdx_rt_reset(void* h) {
   return with_rt(h, [](auto* rt) {
     rt->it = 0;
     rt->x_lag = false;
+    rt->need_import = rt->tiled;  // the new prologue's r and x, at the next iterate
     return 0;
   });
 }
@@ -862,6 +953,7 @@ int bdx_rt_bind_x(void* h, void* x) {
       const hipError_t e = hipStreamSynchronize(rt->st);
       rt->drop_graphs();
       rt->x = static_cast<T*>(x);
+      if (!rt->tiled) rt->wx = rt->x;
       return static_cast<int>(e);
     }
     return 0;

@@ -9,6 +9,14 @@
 //   [12..14] gh 1 if the upper plane of the axis is a ghost plane
 //   [15]    P   polynomial degree
 //   [16]    ld  z pitch of the storage (>= L[2], rows 128-byte aligned)
+//   [17..20] tiled storage (0 = the lattice layout above): tile node sizes
+//           tsy, tsz, storage tiles along z tntz, and the tile-column
+//           stride tcol = L[0] tsy tsz.  In the tiled layout node (i, j, k)
+//           lives at ((j / tsy) tntz + k / tsz) tcol + i tsy tsz
+//           + (j % tsy) tsz + k % tsz: a (y, z) tile's patch of an x-plane
+//           is contiguous (the CG runtime's layout for the x-march kernels,
+//           whose writes of 96-byte row segments ran at 1.7 TB/s in the
+//           lattice layout and 5.4 TB/s tiled, profiles/r2_march_bw.md).
 //
 // The mesh is a structured lattice by construction (see fem/mesh.py), so the
 // cell -> dof map is arithmetic: dof(c, i, j, k) = lattice index
@@ -31,6 +39,7 @@ struct BdxLattice {
   int64_t gh[3];
   int64_t P;
   int64_t ld;
+  int64_t tsy, tsz, tntz, tcol;  // tiled storage (tsy = 0: lattice layout)
 
   static BdxLattice from(const int64_t* d) {
     BdxLattice l;
@@ -43,13 +52,26 @@ struct BdxLattice {
     }
     l.P = d[15];
     l.ld = d[16];
+    l.tsy = d[17];
+    l.tsz = d[18];
+    l.tntz = d[19];
+    l.tcol = d[20];
     return l;
   }
 
+  // lattice-layout index (every lattice kernel)
   BDX_HD int64_t idx(int64_t i, int64_t j, int64_t k) const {
     return (i * L[1] + j) * ld + k;
   }
-  BDX_HD int64_t size() const { return L[0] * L[1] * ld; }
+  // storage index in whichever layout the descriptor selects (the kernels
+  // that also run on the CG runtime's tiled storage)
+  BDX_HD int64_t sidx(int64_t i, int64_t j, int64_t k) const {
+    if (tsy) return ((j / tsy) * tntz + k / tsz) * tcol + (i * tsy + j % tsy) * tsz + k % tsz;
+    return (i * L[1] + j) * ld + k;
+  }
+  BDX_HD int64_t size() const {
+    return tsy ? ((L[1] - 1) / tsy + 1) * tntz * tcol : L[0] * L[1] * ld;
+  }
   // Dirichlet dof: on the boundary of the global unit cube.
   BDX_HD bool is_bc(int64_t i, int64_t j, int64_t k) const {
     int64_t gi = g0[0] + i, gj = g0[1] + j, gk = g0[2] + k;

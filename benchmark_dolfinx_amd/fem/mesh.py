@@ -179,10 +179,20 @@ class LocalLattice:
     def nstore(self) -> int:
         return self.L[0] * self.L[1] * self.ld
 
-    def as_int64(self) -> np.ndarray:
-        """Packed descriptor passed to native code (layout: csrc/include/bdx_lattice.h)."""
+    def as_int64(self, tile: tuple[int, int] | None = None) -> np.ndarray:
+        """Packed descriptor passed to native code (layout: csrc/include/bdx_lattice.h).
+        `tile` = (tsy, tsz) node sizes selects the tiled storage layout."""
+        tl = [0, 0, 0, 0]
+        if tile is not None:
+            tsy, tsz = tile
+            tl = [tsy, tsz, (self.L[2] - 1) // tsz + 1, self.L[0] * tsy * tsz]
         return np.array(list(self.n) + list(self.L) + list(self.g0) + list(self.N)
-                        + list(self.gh) + [self.degree, self.ld], dtype=np.int64)
+                        + list(self.gh) + [self.degree, self.ld] + tl, dtype=np.int64)
+
+    def tiled_size(self, tsy: int, tsz: int) -> int:
+        """Elements of a vector in the tiled storage layout (tiles of tsy x tsz
+        nodes, each tile's x-column contiguous; bdx_lattice.h)."""
+        return ((self.L[1] - 1) // tsy + 1) * ((self.L[2] - 1) // tsz + 1) * self.L[0] * tsy * tsz
 
     # ------------------------------------------------------------- topology
     def rank_of(self, coord) -> int:

@@ -28,6 +28,8 @@ def declare(lib) -> None:
         _d(lib, f"bdx_p_update_{suf}", [i64, i64, i64, i64, i64, vp, vp, vp, i32, i32, vp])
         _d(lib, f"bdx_axpy_{suf}", [i64, i64, i64, i64, i64, vp, f64, vp, vp, vp])
         _d(lib, f"bdx_box_copy_{suf}", [i32, vp, i64, i64, vp, i32, i64, vp, vp])
+        _d(lib, f"bdx_box_copy_lat_{suf}", [i32, vp, vp, vp, i32, i64, vp, vp])
+        _d(lib, f"bdx_layout_convert_{suf}", [i32, vp, vp, vp, vp])
         _d(lib, f"bdx_v1_apply_{suf}",
            [i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp, vp])
         _d(lib, f"bdx_geometry_{suf}", [vp, i32, vp, vp, vp, vp, vp, vp, vp])
@@ -71,7 +73,8 @@ def declare(lib) -> None:
     _d(lib, "bdx_rt_nccl_unique_id", [vp])
     _d(lib, "bdx_rt_rccl_selftest", [vp, i32, vp])
     _d(lib, "bdx_rt_create", [i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
-                              i64, vp], vp)
+                              i64, vp, vp, vp], vp)
+    _d(lib, "bdx_rt_tiled", [vp])
     _d(lib, "bdx_rt_connect", [vp, vp, i32])
     _d(lib, "bdx_rt_comm_count", [vp])
     _d(lib, "bdx_rt_overlap", [vp])

@@ -81,6 +81,18 @@ class NativeCGRuntime:
                                  device=pb.device)
         fo, gh = halo.owned_faces, halo.ghosts
         self.x = cg.x
+        # Tiled vector storage for the x-march kernels (fused4 / fused5): each
+        # (y, z) tile's patch of an x-plane is contiguous, so the kernels'
+        # writes are whole lines (profiles/r2_march_bw.md).  BDX_TILED=0: the
+        # lattice layout.
+        self.tiled = (op.version in (4, 5) and os.environ.get("BDX_TILED", "1") != "0")
+        self._latdT = None
+        self._tbufs = []
+        if self.tiled:
+            self._latdT = np.ascontiguousarray(pb.lat.as_int64((op.sy, op.sz)), dtype=np.int64)
+            n = pb.lat.tiled_size(op.sy, op.sz)
+            self._tbufs = [torch.zeros(n, dtype=pb.dtype, device=pb.device) for _ in range(5)]
+        self._tptrs = (ctypes.c_void_p * 5)(*[ptr(b) for b in self._tbufs]) if self.tiled else None
         bufs = [cg.x, cg.r, op.p_old, op.p_new, cg.y, op.yb, op.zb, op.cb, pb.xv, cg.scal,
                 op.partials, self.upart, halo.buf_a, halo.buf_b, fo.table, gh.table, pb.kc]
         self._keep = bufs + [op.tabs]
@@ -106,7 +118,7 @@ class NativeCGRuntime:
                 int(pb.dtype == torch.float64), ptr(self._latd), ptr(self._own), ptr(self._ip),
                 float(pb.kappa), ptr(self._wts), ptr(self._qpts), ptr(op.tabs), self._ptrs,
                 ptr(self._hs), ptr(self._fc), ptr(self._gc), transport, comm.size, comm.rank,
-                self.group, _stream())
+                self.group, _stream(), ptr(self._latdT), self._tptrs)
             ok = bool(self.h)
         if not _agree(comm, ok):
             self.close()
@@ -130,6 +142,7 @@ class NativeCGRuntime:
                 self.close()
                 raise NativeRuntimeUnavailable("ncclCommInitRank failed on at least one rank")
         self.overlap = bool(self.lib.bdx_rt_overlap(self.h))
+        self.tiled = bool(self.lib.bdx_rt_tiled(self.h))
         self.graphs = False
 
     def comm_ranks(self) -> int:
