@@ -31,10 +31,20 @@ enum { kGeomStored = 0, kGeomOTF = 1 };
 #define BDX_DEBUG 0
 #endif
 #if BDX_DEBUG
-#include <cassert>
-#define BDX_DASSERT(c) assert(c)
+// report (do not trap: a trapped wave would take the queue down with it)
+#define BDX_DASSERT(c) \
+  ((c) ? (void)0 : (void)printf("[bdx ASSERT] %s:%d %s\n", __FILE__, __LINE__, #c))
+// out-of-range global offset: print the first few offenders, skip the access
+#define BDX_OOB(off, n, tag)                                                        \
+  (((off) < 0 || (off) >= (n))                                                      \
+       ? (printf("[bdx OOB] %s off=%lld n=%lld block=%d thread=%d\n", tag,          \
+                 static_cast<long long>(off), static_cast<long long>(n),            \
+                 static_cast<int>(blockIdx.x), static_cast<int>(threadIdx.x)),      \
+          true)                                                                     \
+       : false)
 #else
 #define BDX_DASSERT(c) ((void)0)
+#define BDX_OOB(off, n, tag) false
 #endif
 
 // Streamed vectors (read or written once per CG iteration; every vector is

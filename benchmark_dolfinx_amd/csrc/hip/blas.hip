@@ -173,6 +173,9 @@ __global__ void __launch_bounds__(kBlock)
     // divisions by run-time tile sizes; enumerate lattice order instead (the
     // lattice side then streams, the tiled side moves in 8..16-node runs)
     const int64_t k = e % L2, r = e / L2, j = r % L1v, i = r / L1v;
+    if (BDX_OOB(til(i, j, k), til.tsy ? ((L1v - 1) / til.tsy + 1) * til.tntz * til.tcol : n,
+                "layout convert"))
+      continue;
     if (dir == 0)
       t[til(i, j, k)] = a[lat(i, j, k)];
     else

@@ -221,6 +221,7 @@ __global__ void __launch_bounds__(256)
     const int tY = static_cast<int>(blk / tntz), tZ = static_cast<int>(blk - static_cast<int64_t>(tY) * tntz);
     if (x >= o0) continue;
     const int ein = static_cast<int>(e0 - c * ch);
+    if (BDX_OOB(e0 + W - 1, nvec * W, "tiled update")) continue;
     const V vy = *reinterpret_cast<const V*>(y + e0);
     V vr = *reinterpret_cast<const V*>(r + e0);
     bool any = false;

@@ -83,6 +83,8 @@ struct Fused2Args {
   // tile's column base plus the in-tile position (fused4 / fused5 only)
   int tsy, tsz, tntz;
   int64_t tcol;
+  int64_t vsize;   // elements of one vector (BDX_DEBUG bounds checks)
+  int64_t ibsize;  // elements of the interface buffers yb / zb / cb (max of the three)
 };
 
 // (y, z) part of a vector offset (the x-plane part is x * ps)
@@ -781,6 +783,7 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
   a.tsz = static_cast<int>(L.tsz);
   a.tntz = static_cast<int>(L.tntz);
   a.tcol = L.tcol;
+  a.vsize = L.size();
   if (L.tsy) {
     // tiled: in-tile offsets are whole-vector offsets, still 32-bit
     if (L.size() >= (int64_t(1) << 31) || L.tsz <= 0) return static_cast<int>(hipErrorInvalidValue);
@@ -789,6 +792,10 @@ inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int 
   a.ybps = static_cast<int64_t>(nty - 1) * L.L[2];
   a.zbps = L.L[1] * static_cast<int64_t>(ntz - 1);
   a.cbps = static_cast<int64_t>(nty - 1) * (ntz - 1);
+  {
+    const int64_t y_ = L.L[0] * a.ybps, z_ = L.L[0] * a.zbps, c_ = L.L[0] * a.cbps;
+    a.ibsize = y_ > z_ ? (y_ > c_ ? y_ : c_) : (z_ > c_ ? z_ : c_);
+  }
   a.vps = (L.n[1] + 1) * (L.n[2] + 1) * 3;
   a.ncx = static_cast<int>(L.n[0]);
   a.n1 = static_cast<int>(L.n[1]);

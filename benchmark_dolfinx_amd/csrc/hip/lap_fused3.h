@@ -699,6 +699,9 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
           if (kind == 0) continue;  // Dirichlet y was written at staging
           v = T(0);
         }
+        if (BDX_OOB(lbase * (kind == 0 ? A.ps : kind == 1 ? A.ybps : kind == 2 ? A.zbps : A.cbps) +
+                        ooff, kind == 0 ? A.vsize : A.ibsize, "f3 gather store"))
+          continue;
         T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
         dst[ooff] = v;
       }

@@ -207,6 +207,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     T v;
     if (!wr) f &= ~kOwnT;
     if constexpr (MODE == kFusedCG) {
+      if (BDX_OOB((ul - A.u) + goff, A.vsize, "stage")) return T(0);
       const T po = A.pold[(ul - A.u) + goff];
       v = ul[goff] + beta * po;
       if (xupd && (f & kOwnT)) {
@@ -215,6 +216,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       }
       if (f & kOwnT) pn[goff] = v;
     } else {
+      if (BDX_OOB((ul - A.u) + goff, A.vsize, "stage")) return T(0);
       v = ul[goff];
     }
     (void)pn;
@@ -375,6 +377,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       f.p[k] = T(0);
       f.x[k] = T(0);
       if constexpr ((BDX_F4_DROP & 4) == 0) {
+        if (BDX_OOB(lpf + st_goff[k], A.vsize, "f4 prefetch")) continue;
         f.r[k] = ld_stream(A.u + lpf + st_goff[k]);
         if constexpr (MODE == kFusedCG) {
           f.p[k] = ld_stream(A.pold + lpf + st_goff[k]);
@@ -621,7 +624,9 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
           if (kind == 0) continue;  // Dirichlet y was written at staging
           v = T(0);
         }
-        BDX_DASSERT(o_off[k] >= 0 && (kind != 0 || o_off[k] < (P + 1) * A.ps));
+        if (BDX_OOB(lbase * (kind == 0 ? A.ps : kind == 1 ? A.ybps : kind == 2 ? A.zbps : A.cbps) +
+                        o_off[k], kind == 0 ? A.vsize : A.ibsize, "f4 gather store"))
+          continue;
         if (kind == 0)
           st_stream(ybase[0] + o_off[k], v);
         else
@@ -637,6 +642,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       for (int k = 0; k < NPF; ++k) {
         const int m = st_meta[k];
         if (tid + k * NT < P * PL && (m & kValid) && (m & kOwnT)) {
+          if (BDX_OOB(lnext + st_goff[k], A.vsize, "f4 staging store")) continue;
           const int gxx = (cx + 1) * P + ((m >> 4) & 15);
           if constexpr (MODE == kFusedCG) {
             st_stream(pnl + st_goff[k], pf_r[k]);

@@ -211,6 +211,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     T v;
     if (!wr) f &= ~kOwnT;
     if constexpr (MODE == kFusedCG) {
+      if (BDX_OOB((ul - A.u) + goff, A.vsize, "stage")) return T(0);
       const T po = A.pold[(ul - A.u) + goff];
       v = ul[goff] + beta * po;
       if (xupd && (f & kOwnT)) {
@@ -219,6 +220,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       }
       if (f & kOwnT) pn[goff] = v;
     } else {
+      if (BDX_OOB((ul - A.u) + goff, A.vsize, "stage")) return T(0);
       v = ul[goff];
     }
     (void)pn;
@@ -420,6 +422,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       pf_p[k] = T(0);
       pf_x[k] = T(0);
       if (!(BDX_F5_DROP & 4) && !last && (st_meta[k] & kValid)) {
+        if (BDX_OOB(lnext + st_goff[k], A.vsize, "f5 prefetch")) continue;
         pf_r[k] = ld_stream(un_r + st_goff[k]);
         if constexpr (MODE == kFusedCG) {
           pf_p[k] = ld_stream(un_p + st_goff[k]);
@@ -705,7 +708,9 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
           if (kind == 0) continue;  // Dirichlet y was written at staging
           v = T(0);
         }
-        BDX_DASSERT(o_off[k] >= 0 && (kind != 0 || o_off[k] < (P + 1) * A.ps));
+        if (BDX_OOB(lbase * (kind == 0 ? A.ps : kind == 1 ? A.ybps : kind == 2 ? A.zbps : A.cbps) +
+                        o_off[k], kind == 0 ? A.vsize : A.ibsize, "f5 gather store"))
+          continue;
         if (kind == 0)
           st_stream(ybase[0] + o_off[k], v);
         else
@@ -725,8 +730,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       for (int k = 0; k < NPF; ++k) {
         const int m = st_meta[k];
         if (tid + k * NT < P * PL) {
+          bool m_skip = false;
           T v = T(0);
-          if (m & kValid) {
+          if ((m & kValid) && BDX_OOB(lnext + st_goff[k], A.vsize, "f5 staging store")) m_skip = true;
+          if ((m & kValid) && !m_skip) {
             const int gxx = (cx + 1) * P + ((m >> 4) & 15);
             T val;
             if constexpr (MODE == kFusedCG) {

@@ -84,8 +84,11 @@ class _Done:
 class ThreadGroup:
     """Shared state of an in-process group of ranks (one Python thread each)."""
 
+    _serial = iter(range(1, 1 << 62))  # process-unique group ids (id() gets reused)
+
     def __init__(self, size: int):
         import threading
+        self.uid = next(ThreadGroup._serial)
         self.size = size
         self.barrier = threading.Barrier(size)
         self.slots = [None] * size

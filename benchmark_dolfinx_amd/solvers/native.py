@@ -105,7 +105,8 @@ class NativeCGRuntime:
             transport = 0
         elif hasattr(comm, "g"):  # ThreadComm: ranks are threads of this process
             transport = 2
-            self.group = id(comm.g)
+            self.group = comm.g.uid  # unique per group: a reused id() could
+            # pick up a stale group of a runtime that was not closed yet
         elif comm.backend == "nccl":
             transport = 1
         else:

@@ -107,7 +107,7 @@ def test_bc_mask_and_lattice():
     assert m.sum() == np.prod(lat.L) - np.prod([L - 2 for L in lat.L])
     assert lat.ld % 16 == 0 and lat.ld >= lat.L[2]
     d = lat.as_int64()
-    assert d.dtype == np.int64 and d.size == 17
+    assert d.dtype == np.int64 and d.size == 21
 
 
 @pytest.mark.parametrize("R", [2, 4, 8])
