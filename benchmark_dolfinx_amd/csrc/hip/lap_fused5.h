@@ -38,6 +38,7 @@
 // x update, Dirichlet identity rows, p.Ap partials as element dots) and the
 // atomic-free gather with tile-interface buffers -- is fused4's.
 #pragma once
+#include <cmath>
 #include <cstdlib>
 
 #include "lap_fused2.h"
@@ -51,9 +52,28 @@
 #define BDX_F5_DROP 0
 #endif
 
-// table layout: M, K, C, C^T as 8 x 8 row-major blocks
+// table layout: M, K, C, C^T as 8 x 8 row-major blocks, then the even-odd
+// forms of M and K (4 x 4 blocks at kF5EO + 32 id: E, then O at + 16)
 constexpr int kF5Stride = 8;
-constexpr int kF5Tab = 4 * 64;
+constexpr int kF5EO = 4 * 64;
+constexpr int kF5Tab = kF5EO + 2 * 32;
+// Even-odd decomposition of the centrosymmetric M and K (M[i][j] =
+// M[nd-1-i][nd-1-j] for the symmetric GLL / Gauss rules; checked on the
+// host): out = M in costs ceil(nd/2) x ceil(nd/2) + floor(nd/2)^2 FMAs
+// instead of nd^2 (31 instead of 49 at nd = 7) and half the scalar table
+// loads.  BDX_F5_EO=0 keeps the plain row products (A/B).
+#ifndef BDX_F5_EO
+#define BDX_F5_EO 1
+#endif
+// passes that use it (bit 1 x, 2 z, 4 y) per precision: FP32 all (+11 % at
+// Q6 in a same-box A/B); FP64 all passes spilled 10 dwords in the CG
+// instance and lost 4.6 %, so FP64 takes the subset BDX_F5_EO_F64
+#ifndef BDX_F5_EO_F32
+#define BDX_F5_EO_F32 7
+#endif
+#ifndef BDX_F5_EO_F64
+#define BDX_F5_EO_F64 5
+#endif
 static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
 
 // cells per wave and (y, z) tile per degree; NARR = 4 (sheared cells) keeps
@@ -381,7 +401,45 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     }
   }
   T d1 = T(0), d2 = T(0);
-  auto matvec = [&](int id, const T (&in)[ND], T (&out)[ND], T s, bool acc) {
+  constexpr int EOM = BDX_F5_EO ? (sizeof(T) == 4 ? BDX_F5_EO_F32 : BDX_F5_EO_F64) : 0;
+  auto matvec = [&](int id, const T (&in)[ND], T (&out)[ND], T s, bool acc, int pass) {
+    if constexpr (EOM != 0) {
+      if (id < 2 && (EOM & pass)) {  // M or K: even-odd form (compile-time after inlining)
+        constexpr int H = ND / 2, ODD = ND % 2;
+        T ev[H], od[H];
+#pragma unroll
+        for (int b = 0; b < H; ++b) {
+          ev[b] = in[b] + in[ND - 1 - b];
+          od[b] = in[b] - in[ND - 1 - b];
+        }
+#pragma unroll
+        for (int a = 0; a < H + ODD; ++a) {
+          CT* re = tab0 + kF5EO + id * 32 + a * 4;
+          asm volatile("" : "+s"(re) : "v"(d2));
+          T te = T(0);
+#pragma unroll
+          for (int b = 0; b < H; ++b) te += re[b] * ev[b];
+          if constexpr (ODD) te += re[H] * in[H];
+          if (a < H) {
+            CT* ro = tab0 + kF5EO + id * 32 + 16 + a * 4;
+            asm volatile("" : "+s"(ro) : "v"(d2));
+            T to = T(0);
+#pragma unroll
+            for (int b = 0; b < H; ++b) to += ro[b] * od[b];
+            const T r1 = te + to, r2 = te - to;
+            out[a] = acc ? out[a] + s * r1 : s * r1;
+            out[ND - 1 - a] = acc ? out[ND - 1 - a] + s * r2 : s * r2;
+            d2 = d1;
+            d1 = r1;
+          } else {
+            out[a] = acc ? out[a] + s * te : s * te;
+            d2 = d1;
+            d1 = te;
+          }
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
       CT* row = tab0 + id * 64 + a * kF5Stride;
@@ -587,14 +645,14 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
           for (int i = 0; i < ND; ++i) w[i * ND * NDP] = o[i];
         }
       };
-      matvec(1, u, o, T(1), false);
+      matvec(1, u, o, T(1), false, 1);
       put(0);
-      matvec(0, u, o, T(1), false);
+      matvec(0, u, o, T(1), false, 1);
       put(1);
       if constexpr (MIXED) {
-        matvec(2, u, o, T(1), false);
+        matvec(2, u, o, T(1), false, 1);
         put(2);
-        matvec(3, u, o, T(1), false);
+        matvec(3, u, o, T(1), false, 1);
         put(3);
       }
     }
@@ -607,20 +665,20 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       ldrow<ND>(r, ak);
       ldrow<ND>(r + ARR, am);
       T zM[ND], zK[ND];
-      matvec(0, ak, zM, G00, false);
-      matvec(1, am, zM, G22, true);
-      matvec(0, am, zK, G11, false);
+      matvec(0, ak, zM, G00, false, 2);
+      matvec(1, am, zM, G22, true, 2);
+      matvec(0, am, zK, G11, false, 2);
       if constexpr (MIXED) {
         T ac[ND], at[ND];
         ldrow<ND>(r + 2 * ARR, ac);
         ldrow<ND>(r + 3 * ARR, at);
         T zCt[ND], zC[ND];
-        matvec(3, ac, zM, G02, true);
-        matvec(2, at, zM, G02, true);
-        matvec(0, ac, zCt, G01, false);
-        matvec(2, am, zCt, G12, true);
-        matvec(0, at, zC, G01, false);
-        matvec(3, am, zC, G12, true);
+        matvec(3, ac, zM, G02, true, 2);
+        matvec(2, at, zM, G02, true, 2);
+        matvec(0, ac, zCt, G01, false, 2);
+        matvec(2, am, zCt, G12, true, 2);
+        matvec(0, at, zC, G01, false, 2);
+        matvec(3, am, zC, G12, true, 2);
         wave_sync();
         // rows [i][k][j]: lane (i, j) writes column j of rows (i, k)
         if (lane_on) {
@@ -652,14 +710,14 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       T sM[ND], sK[ND];
       ldrow<ND>(r, sM);
       ldrow<ND>(r + ARR, sK);
-      matvec(0, sM, ye, T(1), false);
-      matvec(1, sK, ye, T(1), true);
+      matvec(0, sM, ye, T(1), false, 4);
+      matvec(1, sK, ye, T(1), true, 4);
       if constexpr (MIXED) {
         T sCt[ND], sC[ND];
         ldrow<ND>(r + 2 * ARR, sCt);
         ldrow<ND>(r + 3 * ARR, sC);
-        matvec(3, sCt, ye, T(1), true);
-        matvec(2, sC, ye, T(1), true);
+        matvec(3, sCt, ye, T(1), true, 4);
+        matvec(2, sC, ye, T(1), true, 4);
       }
     }
     // element dot p_e . (A_e p_e): lane holds y_e[i = la][j][k = lb]
@@ -804,6 +862,33 @@ inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, co
       out[128 + i * kF5Stride + l] = static_cast<T>(c);
       out[192 + l * kF5Stride + i] = static_cast<T>(c);
     }
+  // even-odd forms of M and K (computed in double from the double matrices)
+  for (int id = 0; id < 2; ++id) {
+    double Mx[kF5Stride][kF5Stride];
+    double mx = 0.0;
+    for (int i = 0; i < nd; ++i)
+      for (int l = 0; l < nd; ++l) {
+        double v = 0;
+        for (int q = 0; q < nq; ++q)
+          v += id == 0 ? wts[q] * phi0[q * nd + i] * phi0[q * nd + l]
+                       : wts[q] * Dd[q * nd + i] * Dd[q * nd + l];
+        Mx[i][l] = v;
+        mx = std::fabs(v) > mx ? std::fabs(v) : mx;
+      }
+    for (int i = 0; i < nd; ++i)  // centrosymmetry (symmetric rules): else refuse
+      for (int l = 0; l < nd; ++l)
+        if (std::fabs(Mx[i][l] - Mx[nd - 1 - i][nd - 1 - l]) > 1e-12 * mx) return -2;
+    const int h = nd / 2, odd = nd % 2;
+    T* E = out + kF5EO + id * 32;
+    T* O = E + 16;
+    for (int a = 0; a < h + odd; ++a) {
+      for (int b = 0; b < h; ++b) {
+        E[a * 4 + b] = static_cast<T>(0.5 * (Mx[a][b] + Mx[a][nd - 1 - b]));
+        if (a < h) O[a * 4 + b] = static_cast<T>(0.5 * (Mx[a][b] - Mx[a][nd - 1 - b]));
+      }
+      if (odd) E[a * 4 + h] = static_cast<T>(Mx[a][h]);
+    }
+  }
   return kFusedTabMax;
 }
 

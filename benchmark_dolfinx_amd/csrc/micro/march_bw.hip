@@ -89,6 +89,47 @@ __global__ void __launch_bounds__(NT) march_kernel(Geo g, int mode, double* __re
   if (acc == 12345.678) sink[0] = acc + pin[threadIdx.x];
 }
 
+// In-tile offset of node (ly, lz): row-major (COLFIRST = 0) or with the
+// lz = 0 column stored first (COLFIRST = 1: a tile's first column, which the
+// left neighbour reads as its 13th column, is contiguous).
+template <int COLFIRST>
+__device__ __forceinline__ int intile(int ly, int lz) {
+  if (COLFIRST) return lz == 0 ? ly : TP + ly * (TP - 1) + (lz - 1);
+  return ly * TP + lz;
+}
+
+// Read the operator's 13 x 13 patch of every x-plane (own 12 x 12 plus the
+// neighbours' first row / column) from the tile-major layout.
+template <int COLFIRST>
+__global__ void __launch_bounds__(NT) patch_read_kernel(Geo g, const double* __restrict__ a,
+                                                        double* sink) {
+  __shared__ double pin[LDS_PIN / 8];
+  const int nblk = gridDim.x, ob = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
+  const int ty = bid / g.ntz, tz = bid % g.ntz;
+  constexpr int D = TP + 1, U = 4;
+  const int e = threadIdx.x;
+  const bool on = e < D * D;
+  int ly = e / D, lz = e % D, tyy = ty, tzz = tz;
+  if (ly == TP) { ly = 0; ++tyy; }
+  if (lz == TP) { lz = 0; ++tzz; }
+  const bool in = on && tyy < g.nty && tzz < g.ntz;
+  const long base = (static_cast<long>(tyy) * g.ntz + tzz) * g.X * (TP * TP) + intile<COLFIRST>(ly, lz);
+  double acc = 0.0;
+  for (int x0 = 0; x0 < g.X; x0 += U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int x = x0 + u < g.X ? x0 + u : g.X - 1;
+      v[u] = in ? a[base + static_cast<long>(x) * (TP * TP)] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+  }
+  if (acc == 12345.678) sink[0] = acc + pin[threadIdx.x];
+}
+
 // Flat grid-stride reference: 16 bytes per lane.
 __global__ void __launch_bounds__(NT) stream_kernel(long n, int mode, double* __restrict__ a,
                                                     const double* __restrict__ b, double* sink) {
@@ -152,6 +193,25 @@ int main() {
       std::printf("%-9s %-27s %8.3f ms  %6.2f TB/s\n", mname[mode], kname[kind], best,
                   bytes[mode] / (best * 1e-3) / 1e12);
     }
+  }
+  // the operator's read: 13 x 13 patches (169 reads per 144 owned nodes)
+  for (int cf = 0; cf < 2; ++cf) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; ++rep) {
+      CK(hipEventRecord(t0));
+      if (cf)
+        patch_read_kernel<1><<<tiles, NT>>>(g, a, sink);
+      else
+        patch_read_kernel<0><<<tiles, NT>>>(g, a, sink);
+      CK(hipGetLastError());
+      CK(hipEventRecord(t1));
+      CK(hipEventSynchronize(t1));
+      float ms = 0.f;
+      CK(hipEventElapsedTime(&ms, t0, t1));
+      if (rep > 0 && ms < best) best = ms;
+    }
+    std::printf("patch 13x13 read, tile-major %-22s %8.3f ms  %6.2f TB/s (owned bytes)\n",
+                cf ? "(first column first)" : "(row-major tile)", best, 8.0 * n / (best * 1e-3) / 1e12);
   }
   CK(hipFree(a));
   CK(hipFree(b));
