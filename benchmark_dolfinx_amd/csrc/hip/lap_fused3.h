@@ -44,6 +44,11 @@
 #ifndef BDX_X3_NOSYNC
 #define BDX_X3_NOSYNC 0
 #endif
+// BDX_F3_LAUNDER: per-layer re-materialisation of the gather (bit 1) and
+// staging (bit 2) descriptors (see BDX_F5_LAUNDER in lap_fused5.h)
+#ifndef BDX_F3_LAUNDER
+#define BDX_F3_LAUNDER 3
+#endif
 #ifndef BDX_F3_ORECOMP
 #define BDX_F3_ORECOMP 1
 #endif
@@ -676,6 +681,8 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
           asm volatile("" : "+v"(e));  // recompute here, not hoisted out of the march
           out_desc(e, os0, os1, ooff, m);
         } else {
+          if (BDX_F3_LAUNDER & 1)
+            asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
           os0 = o_src[k][0];
           os1 = o_src[k][1];
           ooff = o_off[k];
@@ -709,6 +716,10 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
 
     // ------------------------------------------------ stage the next layer
     if (!last) {
+      if (BDX_F3_LAUNDER & 2) {
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
+      }
       T* __restrict__ un = s_u[nxt];
 #pragma unroll
       for (int k = 0; k < NCP; ++k)

@@ -34,6 +34,16 @@
 #ifndef BDX_F4_TZ
 #define BDX_F4_TZ 4
 #endif
+// BDX_F4_LAUNDER: re-materialise the per-thread gather (bit 1) / staging
+// (bit 2) descriptors every layer through an empty asm, so the compiler
+// cannot hoist their unpacked fields and flag masks out of the x-march
+// (hoisted, the SGPR masks spill to VGPR lanes: v_readlane per use).
+// Off by default: it removes the loop's 111 v_readlane and 19 VGPRs, but
+// fused4 is LDS-limited to 3 workgroups per CU and a same-box A/B was
+// neutral (52.3 vs 52.6 GDoF/s, profiles/r2_launder.md)
+#ifndef BDX_F4_LAUNDER
+#define BDX_F4_LAUNDER 0
+#endif
 #ifndef BDX_F4_WAVES
 #define BDX_F4_WAVES 3
 #endif
@@ -554,6 +564,10 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     else
       __builtin_amdgcn_s_waitcnt(kWaitNewest);  // pfc landed, pfn in flight
     if (!last) {
+      if (BDX_F4_LAUNDER & 2) {
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
+      }
       T* __restrict__ un = s_u[nxt];
 #pragma unroll
       for (int k = 0; k < NCP; ++k)
@@ -600,6 +614,10 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       const int64_t lbase = static_cast<int64_t>(cx) * P;
       T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
                                   A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
+      if (BDX_F4_LAUNDER & 1) {
+#pragma unroll
+        for (int k = 0; k < NOUT; ++k) asm volatile("" : "+v"(o_off[k]), "+v"(o_meta[k]));
+      }
 #pragma unroll
       for (int k = 0; k < NOUT; ++k) {
         const int m = o_meta[k];

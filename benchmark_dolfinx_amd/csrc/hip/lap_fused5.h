@@ -66,13 +66,24 @@ constexpr int kF5Tab = kF5EO + 2 * 32;
 #define BDX_F5_EO 1
 #endif
 // passes that use it (bit 1 x, 2 z, 4 y) per precision: FP32 all (+11 % at
-// Q6 in a same-box A/B); FP64 all passes spilled 10 dwords in the CG
-// instance and lost 4.6 %, so FP64 takes the subset BDX_F5_EO_F64
+// Q6 in a same-box A/B).  FP64 all passes spilled 10 dwords in the CG
+// instance before the descriptor laundering (BDX_F5_LAUNDER); with it the
+// instance is 188 VGPRs, spill-free, and all passes win (50.4 vs 49.9)
 #ifndef BDX_F5_EO_F32
 #define BDX_F5_EO_F32 7
 #endif
 #ifndef BDX_F5_EO_F64
-#define BDX_F5_EO_F64 5
+#define BDX_F5_EO_F64 7
+#endif
+// BDX_F5_LAUNDER: re-materialise the per-thread gather (bit 1) / staging
+// (bit 2) descriptors every layer through an empty asm, so the compiler
+// cannot hoist their unpacked fields and flag masks out of the x-march
+// (hoisted, they cost ~20 VGPRs and the SGPR masks spill to VGPR lanes)
+#ifndef BDX_F5_LAUNDER
+#define BDX_F5_LAUNDER 3
+#endif
+#ifndef BDX_F5_LBASE
+#define BDX_F5_LBASE 1
 #endif
 static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
 
@@ -378,6 +389,11 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
   // x-march (4 ND^2 doubles would not fit the SGPR file).
   typedef const __attribute__((address_space(4))) T CT;
   CT* const tab0 = (CT*)tabd;
+  // BDX_F5_LBASE: launder one base pointer per row and address the row by a
+  // constant offset (folded into the scalar load's immediate) -- otherwise
+  // the compiler hoists every row pointer out of the x-march and the ~40
+  // SGPR pairs spill to VGPR lanes (v_readlane per use in the loop)
+  CT* tabl = tab0;
   // out[a] (+)= s * sum_b Mat[a][b] in[b]; id 0 = M, 1 = K, 2 = C, 3 = C^T.
   // Row a's pointer is laundered through an asm that consumes the result of
   // row a - 2 (d2): the scalar loads run one row ahead of the FMAs and at
@@ -414,15 +430,26 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
         }
 #pragma unroll
         for (int a = 0; a < H + ODD; ++a) {
-          CT* re = tab0 + kF5EO + id * 32 + a * 4;
-          asm volatile("" : "+s"(re) : "v"(d2));
+          CT* re;
+          if (BDX_F5_LBASE) {
+            asm volatile("" : "+s"(tabl) : "v"(d2));
+            re = tabl + kF5EO + id * 32 + a * 4;
+          } else {
+            re = tab0 + kF5EO + id * 32 + a * 4;
+            asm volatile("" : "+s"(re) : "v"(d2));
+          }
           T te = T(0);
 #pragma unroll
           for (int b = 0; b < H; ++b) te += re[b] * ev[b];
           if constexpr (ODD) te += re[H] * in[H];
           if (a < H) {
-            CT* ro = tab0 + kF5EO + id * 32 + 16 + a * 4;
-            asm volatile("" : "+s"(ro) : "v"(d2));
+            CT* ro;
+            if (BDX_F5_LBASE) {
+              ro = tabl + kF5EO + id * 32 + 16 + a * 4;
+            } else {
+              ro = tab0 + kF5EO + id * 32 + 16 + a * 4;
+              asm volatile("" : "+s"(ro) : "v"(d2));
+            }
             T to = T(0);
 #pragma unroll
             for (int b = 0; b < H; ++b) to += ro[b] * od[b];
@@ -442,8 +469,14 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     }
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
-      CT* row = tab0 + id * 64 + a * kF5Stride;
-      asm volatile("" : "+s"(row) : "v"(d2));
+      CT* row;
+      if (BDX_F5_LBASE) {
+        asm volatile("" : "+s"(tabl) : "v"(d2));
+        row = tabl + id * 64 + a * kF5Stride;
+      } else {
+        row = tab0 + id * 64 + a * kF5Stride;
+        asm volatile("" : "+s"(row) : "v"(d2));
+      }
       T t = T(0);
 #pragma unroll
       for (int b = 0; b < ND; ++b) t += row[b] * in[b];
@@ -739,6 +772,11 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
 
     // ------------------------------------------------ gather-sum and write out
     if constexpr ((BDX_F5_DROP & 2) == 0) {
+      if (BDX_F5_LAUNDER & 1) {
+#pragma unroll
+        for (int k = 0; k < NOUT; ++k)
+          asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
+      }
       const int64_t lbase = static_cast<int64_t>(cx) * P;
       T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
                                   A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
@@ -778,6 +816,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
 
     // ------------------------------------------------ stage the next layer
     if (!last) {
+      if (BDX_F5_LAUNDER & 2) {
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
+      }
       T* __restrict__ un = s_u[nxt];
 #pragma unroll
       for (int k = 0; k < NCP; ++k)
