@@ -48,13 +48,18 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
             # where it does not apply (phi0 = I)
             kernel = "fused3"
         else:
-            # Kronecker cores on parallelepiped meshes (profiles/r1_kernel_ab.md):
-            # fused4 (MFMA) for Q3 FP64 (7.8 ms/iteration vs fused5 8.1, fused3
-            # 12.0), fused5 (nodal sum factorisation) for every other P >= 3
-            # (Q6 FP64 12.1 ms vs fused3 17.8; FP32 8.9 vs 12.4)
+            # Kronecker cores on parallelepiped meshes.  fused5 (nodal sum
+            # factorisation) on axis-aligned boxes at every P >= 3: since the
+            # descriptor laundering (profiles/r2_launder.md) it beats the
+            # fused4 MFMA core at Q3 FP64 (58.4 vs 52.1 GDoF/s, same box,
+            # scripts/job_r2ac.sh).  Sheared parallelepipeds keep fused4 at
+            # Q3 (fused5's 4-array instance halves its occupancy there).
             from .models.fused import fused_supported
-            auto = ("fused4" if fused_supported(pb, 4) else
-                    "fused5" if fused_supported(pb, 5) else "fused3")
+            f5 = fused_supported(pb, 5)
+            if f5 and pb.all_axis_aligned:
+                auto = "fused5"
+            else:
+                auto = ("fused4" if fused_supported(pb, 4) else "fused5" if f5 else "fused3")
             kernel = os.environ.get("BDX_AUTO_AFFINE", auto)
     if kernel == "dofmap":
         # the unstructured data model: explicit cell->dof / cell->vertex maps

@@ -1,8 +1,9 @@
 """Full-size CG iterate pinned across kernel families.
 
 20 CG iterations on the headline meshes (Q3 at 300 M DoFs, Q6 at 500 M DoFs,
-FP64, qmode=1 GLL, one GPU), once with the production operator (fused4 /
-fused5: Kronecker cores, lagged-x / interface-fold CG in the native runtime)
+FP64, qmode=1 GLL, one GPU), once with the production operator (fused5 at
+both degrees, and fused4 at Q3: Kronecker cores, lagged-x / interface-fold CG
+in the native runtime)
 and once with the reference-structured `v1` kernel on stored geometry (G at
 every quadrature point, the layout of src/laplacian.hpp:105-114 and
 src/geometry_gpu.hpp:26-132; plain CG of src/cg.hpp:89-169).  Their iterate
@@ -40,14 +41,15 @@ def _solve(pb, u, kernel, geometry, nits):
     return xn, name
 
 
-@pytest.mark.parametrize("degree,ndofs,prod", [(3, 300_000_000, "fused4"),
-                                               (6, 500_000_000, "fused5")])
-def test_fullsize_cg_iterate_production_vs_stored_geometry(degree, ndofs, prod):
+@pytest.mark.parametrize("degree,ndofs,kernel,prod", [(3, 300_000_000, "auto", "fused5"),
+                                                      (3, 300_000_000, "fused4", "fused4"),
+                                                      (6, 500_000_000, "auto", "fused5")])
+def test_fullsize_cg_iterate_production_vs_stored_geometry(degree, ndofs, kernel, prod):
     torch.cuda.set_device(0)
     nx = compute_mesh_size(ndofs, degree)
     pb = PoissonProblem(Comm(), nx, degree, 1, False, torch.float64, "gpu")
     u = pb.assemble_rhs()
-    x_prod, name_prod = _solve(pb, u, "auto", "auto", 20)
+    x_prod, name_prod = _solve(pb, u, kernel, "auto", 20)
     x_ref, name_ref = _solve(pb, u, "v1", "stored", 20)
     assert name_prod == prod, name_prod
     assert name_ref != name_prod
