@@ -90,7 +90,14 @@ static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
 // cells per wave and (y, z) tile per degree; NARR = 4 (sheared cells) keeps
 // the 2 x 2 tile at ND >= 6 (its per-wave buffers are twice as large)
 template <int ND, int NARR> struct F5Tile;
-template <int NARR> struct F5Tile<4, NARR> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
+#ifndef BDX_F5_TY4
+#define BDX_F5_TY4 4
+#endif
+#ifndef BDX_F5_TZ4
+#define BDX_F5_TZ4 4
+#endif
+template <> struct F5Tile<4, 2> { static constexpr int CPW = 4, TY = BDX_F5_TY4, TZ = BDX_F5_TZ4; };
+template <> struct F5Tile<4, 4> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
 template <int NARR> struct F5Tile<5, NARR> { static constexpr int CPW = 2, TY = 2, TZ = 4; };
 template <int NARR> struct F5Tile<6, NARR> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 #ifndef BDX_F5_TY7
