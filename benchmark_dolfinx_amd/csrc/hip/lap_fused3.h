@@ -52,12 +52,26 @@
 #ifndef BDX_F3_ORECOMP
 #define BDX_F3_ORECOMP 1
 #endif
+#ifndef BDX_F3_GQUNROLL
+#define BDX_F3_GQUNROLL 1
+#endif
 template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 2; };
-// Waves per SIMD the general (trilinear, AFF = 0) instances are compiled for:
-// at NQ = 5 the per-point geometry needs ~250 VGPRs, and forcing the default 3
-// waves spilled 159 dwords (Q3 general 7.7 GDoF/s vs 18.2 at 2 waves, same box)
+// general-geometry instances: BDX_F3_GQUNROLL > 0 overrides the x-loop unroll
+// (rolled: the per-point geometry of one point at a time is live, not NQ)
+// (FP32 at NQ > 5 keeps the 2-way unroll: 34.4 vs 33.9 GDoF/s at Q6)
+template <typename T, int NQ, int AFF> struct QUnroll3G {
+  static constexpr bool on = !AFF && BDX_F3_GQUNROLL > 0 && (sizeof(T) == 8 || NQ <= 5);
+  static constexpr int value = on ? BDX_F3_GQUNROLL : QUnroll3<NQ>::value;
+};
+// Waves per SIMD the general (trilinear, AFF = 0) instances are compiled for.
+// With the fully unrolled per-point x loop the NQ = 5 instance needed ~250
+// VGPRs and 3 waves spilled 159 dwords; with the loop rolled
+// (BDX_F3_GQUNROLL = 1) it is 175 VGPRs at 2 waves and fits 3 waves with an
+// 8-dword spill: Q3 general 18.5 -> 21.4 GDoF/s (same box, job_r2af.sh).
+// LDS caps the P >= 4 instances at 2 workgroups per CU anyway, and there the
+// compiler keeps its 2-wave allocation (no spill).
 #ifndef BDX_FUSED3_GWAVES
-#define BDX_FUSED3_GWAVES 2
+#define BDX_FUSED3_GWAVES 3
 #endif
 template <int NQ, int AFF> struct Fused3Waves {
   static constexpr int value = AFF ? FusedWaves<NQ>::value : BDX_FUSED3_GWAVES;
@@ -500,7 +514,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
     T a1[ND], a2[ND], a3[ND];
 #pragma unroll
     for (int i = 0; i < ND; ++i) a1[i] = a2[i] = a3[i] = T(0);
-BDX_PRAGMA_UNROLL(QUnroll3<NQ>::value)
+BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
     for (int q = 0; q < (BDX_X3_NOXF ? 1 : NQ); ++q) {
       T gxq = 0, gyq = 0, gzq = 0;
 #pragma unroll
