@@ -56,7 +56,11 @@
 // forms of M and K (4 x 4 blocks at kF5EO + 32 id: E, then O at + 16)
 constexpr int kF5Stride = 8;
 constexpr int kF5EO = 4 * 64;
-constexpr int kF5Tab = kF5EO + 2 * 32;
+// packed even-odd rows for FP32 (BDX_F5_PK): row a of id at kF5PK + 32 id +
+// 8 a holds (E[a][b], O[a][b]) pairs, b = 0..3 (odd nd: the middle column
+// E[a][nd/2] in the pair after the last full one, with O = 0)
+constexpr int kF5PK = kF5EO + 2 * 32;
+constexpr int kF5Tab = kF5PK + 2 * 32;
 // Even-odd decomposition of the centrosymmetric M and K (M[i][j] =
 // M[nd-1-i][nd-1-j] for the symmetric GLL / Gauss rules; checked on the
 // host): out = M in costs ceil(nd/2) x ceil(nd/2) + floor(nd/2)^2 FMAs
@@ -81,6 +85,13 @@ constexpr int kF5Tab = kF5EO + 2 * 32;
 // (hoisted, they cost ~20 VGPRs and the SGPR masks spill to VGPR lanes)
 #ifndef BDX_F5_LAUNDER
 #define BDX_F5_LAUNDER 3
+#endif
+// BDX_F5_PK: packed-math (v_pk_fma_f32) even-odd products in the FP32
+// instances.  8 % fewer loop instructions (1406 -> 1295) but neutral in a
+// same-box A/B (Q6 FP32 91.2 vs 91.3 GDoF/s, profiles/r2_launder.md): the
+// FP32 kernel is not VALU-issue-bound, so the scalar form stays the default
+#ifndef BDX_F5_PK
+#define BDX_F5_PK 0
 #endif
 #ifndef BDX_F5_LBASE
 #define BDX_F5_LBASE 1
@@ -426,6 +437,41 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
   T d1 = T(0), d2 = T(0);
   constexpr int EOM = BDX_F5_EO ? (sizeof(T) == 4 ? BDX_F5_EO_F32 : BDX_F5_EO_F64) : 0;
   auto matvec = [&](int id, const T (&in)[ND], T (&out)[ND], T s, bool acc, int pass) {
+    if constexpr (EOM != 0 && BDX_F5_PK && sizeof(T) == 4) {
+      if (id < 2 && (EOM & pass)) {
+        // FP32 even-odd with packed math: (even, odd) sums of a line pair in
+        // one v_pk_add_f32, (E, O) row products in v_pk_fma_f32 against the
+        // interleaved table rows (one SGPR pair per product)
+        typedef float F2 __attribute__((ext_vector_type(2)));
+        typedef const __attribute__((address_space(4))) F2 CF2;
+        constexpr int H = ND / 2, ODD = ND % 2;
+        F2 eo[H];
+#pragma unroll
+        for (int b = 0; b < H; ++b) eo[b] = F2{in[b], in[b]} + F2{in[ND - 1 - b], -in[ND - 1 - b]};
+#pragma unroll
+        for (int a = 0; a < H + ODD; ++a) {
+          asm volatile("" : "+s"(tabl) : "v"(d2));
+          CF2* rp = reinterpret_cast<CF2*>(tabl + kF5PK + id * 32 + a * 8);
+          F2 t2 = rp[0] * eo[0];
+#pragma unroll
+          for (int b = 1; b < H; ++b) t2 = rp[b] * eo[b] + t2;
+          T te = t2.x;
+          if constexpr (ODD) te += rp[H].x * in[H];
+          if (a < H) {
+            const T r1 = te + t2.y, r2 = te - t2.y;
+            out[a] = acc ? out[a] + s * r1 : s * r1;
+            out[ND - 1 - a] = acc ? out[ND - 1 - a] + s * r2 : s * r2;
+            d2 = d1;
+            d1 = r1;
+          } else {
+            out[a] = acc ? out[a] + s * te : s * te;
+            d2 = d1;
+            d1 = te;
+          }
+        }
+        return;
+      }
+    }
     if constexpr (EOM != 0) {
       if (id < 2 && (EOM & pass)) {  // M or K: even-odd form (compile-time after inlining)
         constexpr int H = ND / 2, ODD = ND % 2;
@@ -936,6 +982,14 @@ inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, co
         if (a < h) O[a * 4 + b] = static_cast<T>(0.5 * (Mx[a][b] - Mx[a][nd - 1 - b]));
       }
       if (odd) E[a * 4 + h] = static_cast<T>(Mx[a][h]);
+    }
+    T* PK = out + kF5PK + id * 32;
+    for (int a = 0; a < h + odd; ++a) {
+      for (int b = 0; b < h; ++b) {
+        PK[a * 8 + 2 * b] = E[a * 4 + b];
+        PK[a * 8 + 2 * b + 1] = a < h ? O[a * 4 + b] : T(0);
+      }
+      if (odd) PK[a * 8 + 2 * h] = E[a * 4 + h];
     }
   }
   return kFusedTabMax;
