@@ -152,7 +152,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
   const int cend = (sa + A.seglen < A.ncx) ? sa + A.seglen : A.ncx;
   const int cbeg = sa > 0 ? sa - 1 : 0;
   const int y0 = ty * TY * P, z0 = tz * TZ * P;
-  const int Ly = A.Ly, Lz = A.Lz, ld = A.ld;
+  const int Ly = A.Ly, Lz = A.Lz;
   const int ncx = A.ncx;
   const bool top_y = (ty == A.nty - 1), top_z = (tz == A.ntz - 1);
   const int ey = (y0 + DY <= Ly) ? DY : Ly - y0;
@@ -230,7 +230,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
     if (e < P * PL) {
       const int pl = 1 + e / PL, rem = e % PL, ly = rem / DZ, lz = rem % DZ;
       const int f = yz_flags(ly, lz);
-      st_goff[k] = (pl * Ly + y0 + ly) * ld + z0 + lz;
+      st_goff[k] = static_cast<int>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz));
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
   }
@@ -261,7 +261,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
         int kind, off;
         if (iy && iz) {
           kind = 0;
-          off = (pl * Ly + gy) * ld + gz;
+          off = static_cast<int>(pl * A.ps + fused_yzoff(A, gy, gz));
         } else if (!iy && iz) {
           kind = 1;
           off = static_cast<int>(pl * A.ybps) + ty * Lz + gz;
@@ -319,7 +319,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
       T v = T(0);
       if (f & kValid)
         v = stage(f, cbeg * P + pl, A.u + l0, A.pnew + l0, A.y + l0,
-                  (pl * Ly + y0 + ly) * ld + z0 + lz, wr);
+                  static_cast<int>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz)), wr);
       s_u[0][pl * PLP + ly * DZP + lz] = v;
     }
   }
@@ -836,7 +836,6 @@ int fused3_resident(int affine) {
       int nty, int ntz, const int* rect, hipStream_t st) {                                          \
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
-    if (a.tsy) return static_cast<int>(hipErrorInvalidValue); /* lattice layout only */ \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
     BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
     mode &= 0xff;                                                                  \

@@ -751,7 +751,7 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   rt->tiled = c.latdT[17] != 0;
   if (rt->tiled) {
     // only the x-march kernels whose tile is the storage tile address it
-    if ((c.version != 4 && c.version != 5) || c.latdT[17] != c.sy || c.latdT[18] != c.sz)
+    if ((c.version < 3 || c.version > 5) || c.latdT[17] != c.sy || c.latdT[18] != c.sz)
       return nullptr;
     rt->xt = static_cast<T*>(tptrs[0]);
     rt->rt_ = static_cast<T*>(tptrs[1]);

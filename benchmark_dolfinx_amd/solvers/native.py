@@ -81,11 +81,17 @@ class NativeCGRuntime:
                                  device=pb.device)
         fo, gh = halo.owned_faces, halo.ghosts
         self.x = cg.x
-        # Tiled vector storage for the x-march kernels (fused4 / fused5): each
-        # (y, z) tile's patch of an x-plane is contiguous, so the kernels'
-        # writes are whole lines (profiles/r2_march_bw.md).  BDX_TILED=0: the
-        # lattice layout.
-        self.tiled = (op.version in (4, 5) and os.environ.get("BDX_TILED", "1") != "0")
+        # Tiled vector storage for the x-march kernels: each (y, z) tile's
+        # patch of an x-plane is contiguous, so the kernels' writes are whole
+        # lines (profiles/r2_march_bw.md).  BDX_TILED=0: the lattice layout;
+        # 1 (default): fused4 / fused5; 2: fused3 as well (the general-geometry
+        # kernel is compute-bound: Q3 +0.6 %, Q6 -2.4 % on tiled storage,
+        # profiles/r2_launder.md).  The tiled r update needs 16-byte tile
+        # planes.
+        mode = os.environ.get("BDX_TILED", "1")
+        esz = 8 if pb.dtype == torch.float64 else 4
+        self.tiled = (mode != "0" and (op.version in (4, 5) or (op.version == 3 and mode == "2"))
+                      and (op.sy * op.sz * esz) % 16 == 0)
         self._latdT = None
         self._tbufs = []
         if self.tiled:

@@ -179,8 +179,8 @@ def test_bench_entry_point_one_gpu():
     assert np.isfinite(cfg["y_norm"]) and cfg["y_norm"] > 0
 
 
-def _tiled_job(comm, nc, P, nreps, version, dtype, coef, shear=0.0):
-    pb = PoissonProblem(comm, nc, P, 1, False, dtype, "gpu", 0.0, coef, shear,
+def _tiled_job(comm, nc, P, nreps, version, dtype, coef, shear=0.0, pert=0.0):
+    pb = PoissonProblem(comm, nc, P, 1, False, dtype, "gpu", pert, coef, shear,
                         partition="yz")
     u = pb.assemble_rhs()
     x = pb.new_vector()
@@ -223,3 +223,28 @@ def test_tiled_storage_matches_lattice_layout(monkeypatch, version, P, nc, dtype
         assert abs(a1 - b1) <= tol * abs(b1), (a1, b1)
         assert abs(a2 - b2) <= tol * abs(b2), (a2, b2)
         assert abs(a1 - a2) <= tol * abs(a1)  # the re-imported solve repeats the first
+
+
+@pytest.mark.parametrize("P,nc,dtype,coef,pert", [
+    (3, (6, 9, 14), torch.float64, "random", 0.15),
+    (6, (3, 5, 6), torch.float64, "constant", 0.15),
+    (2, (5, 7, 9), torch.float64, "constant", 0.15),
+    (3, (5, 9, 10), torch.float32, "constant", 0.15),
+    (6, (3, 5, 6), torch.float32, "constant", 0.15),
+    (4, (4, 7, 9), torch.float64, "constant", 0.0),
+])
+@pytest.mark.parametrize("ranks", [1, 4])
+def test_tiled_storage_fused3_general(monkeypatch, P, nc, dtype, coef, pert, ranks):
+    """fused3 (general trilinear geometry) on the runtime's tiled storage
+    against the lattice layout, 1 and 4 threaded ranks (opt-in: BDX_TILED=2;
+    an FP32 tile plane that is not a multiple of 16 bytes stays on the
+    lattice layout)."""
+    monkeypatch.setenv("BDX_TILED", "2")
+    got = run_threaded(ranks, _tiled_job, nc, P, 12, 3, dtype, coef, 0.0, pert)
+    monkeypatch.setenv("BDX_TILED", "0")
+    ref = run_threaded(ranks, _tiled_job, nc, P, 12, 3, dtype, coef, 0.0, pert)
+    tol = 1e-11 if dtype == torch.float64 else 2e-4
+    for (a1, a2, t1), (b1, b2, t0) in zip(got, ref):
+        assert t1 is (dtype == torch.float64 or P % 2 == 0) and t0 is False
+        assert abs(a1 - b1) <= tol * abs(b1), (a1, b1)
+        assert abs(a2 - b2) <= tol * abs(b2), (a2, b2)
