@@ -93,6 +93,14 @@ constexpr int kF5Tab = kF5PK + 2 * 32;
 #ifndef BDX_F5_PK
 #define BDX_F5_PK 0
 #endif
+// BDX_F5_ZSPLIT: z pass of the 2-array instance writes zK back before
+// forming zM (fewer live registers at the pass's peak: Q6 FP64 CG instance
+// 188 -> 170 VGPRs; +0.9 % Q6 FP64, +0.6 % Q6 FP32 same box).  The 3-wave
+// builds it enables (164 VGPRs spill-free with even-odd on x/y) measured
+// slower: 50.2 vs 52.5 GDoF/s (profiles/r2_launder.md)
+#ifndef BDX_F5_ZSPLIT
+#define BDX_F5_ZSPLIT 1
+#endif
 #ifndef BDX_F5_LBASE
 #define BDX_F5_LBASE 1
 #endif
@@ -745,7 +753,33 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     wave_sync();
 
     // ------------------------------------------------ z pass: lane (i, j) = (la, lb)
-    if constexpr ((BDX_F5_DROP & 1) == 0) {
+    if constexpr ((BDX_F5_DROP & 1) == 0 && !MIXED && BDX_F5_ZSPLIT) {
+      // both input rows of every lane are in registers once the loads have
+      // returned (one ds_read per row for the whole wave), so zK can be
+      // written back before zM is formed: one output row live, not two
+      const T* r = Wc + ab * NDP;
+      T ak[ND], am[ND];
+      ldrow<ND>(r, ak);
+      ldrow<ND>(r + ARR, am);
+      T* w = Wc + la * ND * NDP + lb;
+      {
+        T zK[ND];
+        matvec(0, am, zK, G11, false, 2);
+        wave_sync();
+        if (lane_on) {
+#pragma unroll
+          for (int k = 0; k < ND; ++k) w[ARR + k * NDP] = zK[k];
+        }
+      }
+      T zM[ND];
+      matvec(0, ak, zM, G00, false, 2);
+      matvec(1, am, zM, G22, true, 2);
+      if (lane_on) {
+#pragma unroll
+        for (int k = 0; k < ND; ++k) w[k * NDP] = zM[k];
+      }
+      wave_sync();
+    } else if constexpr ((BDX_F5_DROP & 1) == 0) {
       const T* r = Wc + ab * NDP;
       T ak[ND], am[ND];
       ldrow<ND>(r, ak);
