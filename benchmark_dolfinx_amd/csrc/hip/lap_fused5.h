@@ -98,6 +98,15 @@ constexpr int kF5Tab = kF5PK + 2 * 32;
 // 188 -> 170 VGPRs; +0.9 % Q6 FP64, +0.6 % Q6 FP32 same box).  The 3-wave
 // builds it enables (164 VGPRs spill-free with even-odd on x/y) measured
 // slower: 50.2 vs 52.5 GDoF/s (profiles/r2_launder.md)
+// BDX_F5_STAGE_FIRST: consume the prefetch (LDS staging and the p / x
+// stores) before the gather's stores, behind one explicit vmcnt(0).  In the
+// other order the prefetch registers are read after the gather's divergent
+// stores, the waitcnt pass cannot count them, and every staging slot waits
+// with vmcnt(0), draining all stores issued before it.  Same box: Q3 +4.1 %,
+// Q6 FP64 +1.1 %, Q6 FP32 +2.8 % (profiles/r2_launder.md)
+#ifndef BDX_F5_STAGE_FIRST
+#define BDX_F5_STAGE_FIRST 1
+#endif
 #ifndef BDX_F5_ZSPLIT
 #define BDX_F5_ZSPLIT 1
 #endif
@@ -857,109 +866,127 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     }
     __syncthreads();
 
-    // ------------------------------------------------ gather-sum and write out
-    if constexpr ((BDX_F5_DROP & 2) == 0) {
-      if (BDX_F5_LAUNDER & 1) {
-#pragma unroll
-        for (int k = 0; k < NOUT; ++k)
-          asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
-      }
-      const int64_t lbase = static_cast<int64_t>(cx) * P;
-      T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
-                                  A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
-#pragma unroll
-      for (int k = 0; k < NOUT; ++k) {
-        const int m = o_meta[k];
-        if (!(m & kValid)) continue;
-        const int pl = (m >> 8) & 15, rem = m >> 12;
-        BDX_DASSERT((o_src[k][0] & 0xffff) <= ZSLOT && (o_src[k][0] >> 16) <= ZSLOT &&
-                    (o_src[k][1] & 0xffff) <= ZSLOT && (o_src[k][1] >> 16) <= ZSLOT && rem < PL);
-        T v = s_w[o_src[k][0] & 0xffff] + s_w[o_src[k][0] >> 16] +
-              s_w[o_src[k][1] & 0xffff] + s_w[o_src[k][1] >> 16];
-        if (pl == 0) v += s_c[cur][rem];
-        if (pl == P && !last) {
-          s_c[nxt][rem] = v;
-          continue;
+    auto do_gather = [&]() __attribute__((always_inline)) {
+      // ------------------------------------------------ gather-sum and write out
+      if constexpr ((BDX_F5_DROP & 2) == 0) {
+        if (BDX_F5_LAUNDER & 1) {
+  #pragma unroll
+          for (int k = 0; k < NOUT; ++k)
+            asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
         }
-        // a redundant layer only carries; a segment's end plane is completed
-        // (and written) by the next segment
-        if (red || (pl == P && !glast)) continue;
-        const int gxx = cx * P + pl;
-        const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
-        const int kind = (m >> 4) & 3;
-        if (bc) {
-          if (kind == 0) continue;  // Dirichlet y was written at staging
-          v = T(0);
+        const int64_t lbase = static_cast<int64_t>(cx) * P;
+        T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
+                                    A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
+  #pragma unroll
+        for (int k = 0; k < NOUT; ++k) {
+          const int m = o_meta[k];
+          if (!(m & kValid)) continue;
+          const int pl = (m >> 8) & 15, rem = m >> 12;
+          BDX_DASSERT((o_src[k][0] & 0xffff) <= ZSLOT && (o_src[k][0] >> 16) <= ZSLOT &&
+                      (o_src[k][1] & 0xffff) <= ZSLOT && (o_src[k][1] >> 16) <= ZSLOT && rem < PL);
+          T v = s_w[o_src[k][0] & 0xffff] + s_w[o_src[k][0] >> 16] +
+                s_w[o_src[k][1] & 0xffff] + s_w[o_src[k][1] >> 16];
+          if (pl == 0) v += s_c[cur][rem];
+          if (pl == P && !last) {
+            s_c[nxt][rem] = v;
+            continue;
+          }
+          // a redundant layer only carries; a segment's end plane is completed
+          // (and written) by the next segment
+          if (red || (pl == P && !glast)) continue;
+          const int gxx = cx * P + pl;
+          const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
+          const int kind = (m >> 4) & 3;
+          if (bc) {
+            if (kind == 0) continue;  // Dirichlet y was written at staging
+            v = T(0);
+          }
+          if (BDX_OOB(lbase * (kind == 0 ? A.ps : kind == 1 ? A.ybps : kind == 2 ? A.zbps : A.cbps) +
+                          o_off[k], kind == 0 ? A.vsize : A.ibsize, "f5 gather store"))
+            continue;
+          if (kind == 0)
+            st_stream(ybase[0] + o_off[k], v);
+          else
+            (kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3])[o_off[k]] = v;
         }
-        if (BDX_OOB(lbase * (kind == 0 ? A.ps : kind == 1 ? A.ybps : kind == 2 ? A.zbps : A.cbps) +
-                        o_off[k], kind == 0 ? A.vsize : A.ibsize, "f5 gather store"))
-          continue;
-        if (kind == 0)
-          st_stream(ybase[0] + o_off[k], v);
-        else
-          (kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3])[o_off[k]] = v;
       }
-    }
 
-    // ------------------------------------------------ stage the next layer
-    if (!last) {
-      if (BDX_F5_LAUNDER & 2) {
-#pragma unroll
-        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
-      }
-      T* __restrict__ un = s_u[nxt];
-#pragma unroll
-      for (int k = 0; k < NCP; ++k)
-        if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
-      T* __restrict__ pnl = A.pnew + lnext;
-      T* __restrict__ yl = A.y + lnext;
-#pragma unroll
-      for (int k = 0; k < NPF; ++k) {
-        const int m = st_meta[k];
-        if (tid + k * NT < P * PL) {
-          bool m_skip = false;
-          T v = T(0);
-          if ((m & kValid) && BDX_OOB(lnext + st_goff[k], A.vsize, "f5 staging store")) m_skip = true;
-          if ((m & kValid) && !m_skip) {
-            const int gxx = (cx + 1) * P + ((m >> 4) & 15);
-            T val;
-            if constexpr (MODE == kFusedCG) {
-              val = pf_r[k] + beta * pf_p[k];
-            } else {
-              val = pf_r[k];
-            }
-            if constexpr (MODE == kFusedCG) {
-              if (m & kOwnT) {
-                st_stream(pnl + st_goff[k], val);
-                if (xupd) st_stream(un_x + st_goff[k], pf_x[k] + xalpha * pf_p[k]);
+    };
+    auto do_stage = [&]() __attribute__((always_inline)) {
+      // ------------------------------------------------ stage the next layer
+      if (!last) {
+        if (BDX_F5_LAUNDER & 2) {
+  #pragma unroll
+          for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
+        }
+        T* __restrict__ un = s_u[nxt];
+  #pragma unroll
+        for (int k = 0; k < NCP; ++k)
+          if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
+        T* __restrict__ pnl = A.pnew + lnext;
+        T* __restrict__ yl = A.y + lnext;
+  #pragma unroll
+        for (int k = 0; k < NPF; ++k) {
+          const int m = st_meta[k];
+          if (tid + k * NT < P * PL) {
+            bool m_skip = false;
+            T v = T(0);
+            if ((m & kValid) && BDX_OOB(lnext + st_goff[k], A.vsize, "f5 staging store")) m_skip = true;
+            if ((m & kValid) && !m_skip) {
+              const int gxx = (cx + 1) * P + ((m >> 4) & 15);
+              T val;
+              if constexpr (MODE == kFusedCG) {
+                val = pf_r[k] + beta * pf_p[k];
+              } else {
+                val = pf_r[k];
               }
-            }
-            if ((m & kBcYZ) || gxx == A.bcx_hi) {
-              if (m & kOwnT) {
-                const bool rown = (m & kRownYZ) && gxx < A.ownx;
-                yl[st_goff[k]] = rown ? val : T(0);
-                if constexpr (MODE == kFusedCG) {
-                  if (rown) pap += static_cast<double>(val) * static_cast<double>(val);
+              if constexpr (MODE == kFusedCG) {
+                if (m & kOwnT) {
+                  st_stream(pnl + st_goff[k], val);
+                  if (xupd) st_stream(un_x + st_goff[k], pf_x[k] + xalpha * pf_p[k]);
                 }
               }
-              val = T(0);
+              if ((m & kBcYZ) || gxx == A.bcx_hi) {
+                if (m & kOwnT) {
+                  const bool rown = (m & kRownYZ) && gxx < A.ownx;
+                  yl[st_goff[k]] = rown ? val : T(0);
+                  if constexpr (MODE == kFusedCG) {
+                    if (rown) pap += static_cast<double>(val) * static_cast<double>(val);
+                  }
+                }
+                val = T(0);
+              }
+              v = val;
             }
-            v = val;
+            BDX_DASSERT((m >> 8) >= 0 && (m >> 8) < ND * PLP);
+            un[m >> 8] = v;
           }
-          BDX_DASSERT((m >> 8) >= 0 && (m >> 8) < ND * PLP);
-          un[m >> 8] = v;
+        }
+  #pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][e] = sX[NV + e];
+        }
+  #pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][NV + e] = pf_v[k];
         }
       }
-#pragma unroll
-      for (int k = 0; k < NPV; ++k) {
-        const int e = tid + k * NT;
-        if (e < NV) s_X[nxt][e] = sX[NV + e];
-      }
-#pragma unroll
-      for (int k = 0; k < NPV; ++k) {
-        const int e = tid + k * NT;
-        if (e < NV) s_X[nxt][NV + e] = pf_v[k];
-      }
+    };
+    // BDX_F5_STAGE_FIRST: consume the prefetch (wait for the loads) before
+    // the gather issues its stores, so the wait does not drain them
+    if constexpr (BDX_F5_STAGE_FIRST) {
+      // one explicit, unconditional vmcnt(0) (gfx9 encoding; expcnt and
+      // lgkmcnt untouched): the prefetch has landed and no store of this
+      // layer is pending yet, so the waitcnt pass sees nothing outstanding
+      // and does not put a draining wait before each slot's stores
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      do_stage();
+      do_gather();
+    } else {
+      do_gather();
+      do_stage();
     }
     kc_cur = kc_nxt;
   }
