@@ -49,6 +49,9 @@
 #ifndef BDX_F3_LAUNDER
 #define BDX_F3_LAUNDER 3
 #endif
+#ifndef BDX_F3_STAGE_FIRST
+#define BDX_F3_STAGE_FIRST 1
+#endif
 #ifndef BDX_F3_ORECOMP
 #define BDX_F3_ORECOMP 1
 #endif
@@ -340,6 +343,13 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
   T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};
   T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};
 
+  // per-cell coefficient: the next layer's value rides with the prefetch
+  // batch (consumed in the same layer, its load made the waitcnt pass drain
+  // the whole batch with a vmcnt(0) in the geometry phase, even with
+  // constant kappa, where the load itself is skipped)
+  const int64_t kc_ps = static_cast<int64_t>(A.n1) * A.n2;
+  const int64_t kc_cell = static_cast<int64_t>(ty * TY + cy) * A.n2 + tz * TZ + cz;
+  T kc_cur = A.kc ? (cell_on ? A.kc[cbeg * kc_ps + kc_cell] : T(0)) : A.kappa;
   for (int cx = cbeg; cx < cend; ++cx) {
     const int cur = (cx - cbeg) & 1, nxt = cur ^ 1;
     const bool last = (cx == cend - 1);   // end of this segment
@@ -351,6 +361,16 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
     const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
     T pf_r[NPF], pf_p[NPF], pf_x[NPF];
     T pf_v[NPV];
+    // vertex plane and coefficient first: the loads whose addresses may come
+    // back from a register spill (and its vmcnt wait) go before the vector
+    // batch, so such a wait cannot drain it
+    T kc_nxt = kc_cur;
+    if (A.kc && !last && cell_on) kc_nxt = A.kc[static_cast<int64_t>(cx + 1) * kc_ps + kc_cell];
+#pragma unroll
+    for (int k = 0; k < NPV; ++k) {
+      pf_v[k] = T(0);
+      if (!last && v_off[k] >= 0) pf_v[k] = A.xv[static_cast<int64_t>(cx + 2) * A.vps + v_off[k]];
+    }
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
       pf_r[k] = T(0);
@@ -363,11 +383,6 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
           if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = A.x[lnext + st_goff[k]];
         }
       }
-    }
-#pragma unroll
-    for (int k = 0; k < NPV; ++k) {
-      pf_v[k] = T(0);
-      if (!last && v_off[k] >= 0) pf_v[k] = A.xv[static_cast<int64_t>(cx + 2) * A.vps + v_off[k]];
     }
 
     int toff = 0;
@@ -457,11 +472,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
     // G = kappa w_a w_b adj(J) adj(J)^T / det J is formed once per thread and
     // layer; per point only the weight w_q remains (same operator, same maths).
     T Gc[6] = {0, 0, 0, 0, 0, 0};
-    const T kcell = A.kc ? (cell_on ? A.kc[(static_cast<int64_t>(cx) * A.n1 + ty * TY + cy) * A.n2 +
-                                          tz * TZ + cz]
-                                    : T(0))
-                         : A.kappa;
-    const T kwyz = kcell * s_qw[NQ + a] * s_qw[NQ + b];
+    const T kwyz = kc_cur * s_qw[NQ + a] * s_qw[NQ + b];
     {
       const T* X0 = sX;
       const T* X1 = sX + NV;
@@ -682,109 +693,124 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
     }
     __syncthreads();
 
-    // ------------------------------------------------ gather-sum and write out
-    {
-      const int64_t lbase = static_cast<int64_t>(cx) * P;
-      T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
-                                  A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
-#pragma unroll
-      for (int k = 0; k < NOUT; ++k) {
-        int os0, os1, ooff, m;
-        if constexpr (ORECOMP) {
-          int e = tid + k * NT;
-          asm volatile("" : "+v"(e));  // recompute here, not hoisted out of the march
-          out_desc(e, os0, os1, ooff, m);
-        } else {
-          if (BDX_F3_LAUNDER & 1)
-            asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
-          os0 = o_src[k][0];
-          os1 = o_src[k][1];
-          ooff = o_off[k];
-          m = o_meta[k];
+    auto do_gather = [&]() __attribute__((always_inline)) {
+      // ------------------------------------------------ gather-sum and write out
+      {
+        const int64_t lbase = static_cast<int64_t>(cx) * P;
+        T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
+                                    A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
+  #pragma unroll
+        for (int k = 0; k < NOUT; ++k) {
+          int os0, os1, ooff, m;
+          if constexpr (ORECOMP) {
+            int e = tid + k * NT;
+            asm volatile("" : "+v"(e));  // recompute here, not hoisted out of the march
+            out_desc(e, os0, os1, ooff, m);
+          } else {
+            if (BDX_F3_LAUNDER & 1)
+              asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
+            os0 = o_src[k][0];
+            os1 = o_src[k][1];
+            ooff = o_off[k];
+            m = o_meta[k];
+          }
+          if (BDX_X_NOOUT || !(m & kValid)) continue;
+          const int pl = (m >> 8) & 15, rem = m >> 12;
+          T v = s_wa[os0 & 0xffff] + s_wa[os0 >> 16] + s_wa[os1 & 0xffff] + s_wa[os1 >> 16];
+          if (pl == 0) v += s_c[cur][rem];
+          if (pl == P && !last) {
+            s_c[nxt][rem] = v;
+            continue;
+          }
+          // a redundant layer only carries; a segment's end plane is completed
+          // (and written) by the next segment
+          if (red || (pl == P && !glast)) continue;
+          const int gxx = cx * P + pl;
+          const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
+          const int kind = (m >> 4) & 3;
+          if (bc) {
+            if (kind == 0) continue;  // Dirichlet y was written at staging
+            v = T(0);
+          }
+          if (BDX_OOB(lbase * (kind == 0 ? A.ps : kind == 1 ? A.ybps : kind == 2 ? A.zbps : A.cbps) +
+                          ooff, kind == 0 ? A.vsize : A.ibsize, "f3 gather store"))
+            continue;
+          T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
+          dst[ooff] = v;
         }
-        if (BDX_X_NOOUT || !(m & kValid)) continue;
-        const int pl = (m >> 8) & 15, rem = m >> 12;
-        T v = s_wa[os0 & 0xffff] + s_wa[os0 >> 16] + s_wa[os1 & 0xffff] + s_wa[os1 >> 16];
-        if (pl == 0) v += s_c[cur][rem];
-        if (pl == P && !last) {
-          s_c[nxt][rem] = v;
-          continue;
-        }
-        // a redundant layer only carries; a segment's end plane is completed
-        // (and written) by the next segment
-        if (red || (pl == P && !glast)) continue;
-        const int gxx = cx * P + pl;
-        const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
-        const int kind = (m >> 4) & 3;
-        if (bc) {
-          if (kind == 0) continue;  // Dirichlet y was written at staging
-          v = T(0);
-        }
-        if (BDX_OOB(lbase * (kind == 0 ? A.ps : kind == 1 ? A.ybps : kind == 2 ? A.zbps : A.cbps) +
-                        ooff, kind == 0 ? A.vsize : A.ibsize, "f3 gather store"))
-          continue;
-        T* __restrict__ dst = kind == 0 ? ybase[0] : kind == 1 ? ybase[1] : kind == 2 ? ybase[2] : ybase[3];
-        dst[ooff] = v;
       }
-    }
 
-    // ------------------------------------------------ stage the next layer
-    if (!last) {
-      if (BDX_F3_LAUNDER & 2) {
-#pragma unroll
-        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
-      }
-      T* __restrict__ un = s_u[nxt];
-#pragma unroll
-      for (int k = 0; k < NCP; ++k)
-        if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
-      T* __restrict__ pnl = A.pnew + lnext;
-      T* __restrict__ yl = A.y + lnext;
-#pragma unroll
-      for (int k = 0; k < NPF; ++k) {
-        const int m = st_meta[k];
-        if (tid + k * NT < P * PL) {
-          T v = T(0);
-          if (m & kValid) {
-            const int gxx = (cx + 1) * P + ((m >> 4) & 15);
-            T val;
-            if constexpr (MODE == kFusedCG) {
-              val = pf_r[k] + beta * pf_p[k];
-            } else {
-              val = pf_r[k];
-            }
-            if constexpr (MODE == kFusedCG) {
-              if (m & kOwnT) {
-                pnl[st_goff[k]] = val;
-                if (xupd) A.x[lnext + st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
+    };
+    auto do_stage = [&]() __attribute__((always_inline)) {
+      // ------------------------------------------------ stage the next layer
+      if (!last) {
+        if (BDX_F3_LAUNDER & 2) {
+  #pragma unroll
+          for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
+        }
+        T* __restrict__ un = s_u[nxt];
+  #pragma unroll
+        for (int k = 0; k < NCP; ++k)
+          if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
+        T* __restrict__ pnl = A.pnew + lnext;
+        T* __restrict__ yl = A.y + lnext;
+  #pragma unroll
+        for (int k = 0; k < NPF; ++k) {
+          const int m = st_meta[k];
+          if (tid + k * NT < P * PL) {
+            T v = T(0);
+            if (m & kValid) {
+              const int gxx = (cx + 1) * P + ((m >> 4) & 15);
+              T val;
+              if constexpr (MODE == kFusedCG) {
+                val = pf_r[k] + beta * pf_p[k];
+              } else {
+                val = pf_r[k];
               }
-            }
-            if ((m & kBcYZ) || gxx == A.bcx_hi) {
-              if (m & kOwnT) {
-                const bool rown = (m & kRownYZ) && gxx < A.ownx;
-                yl[st_goff[k]] = rown ? val : T(0);
-                if constexpr (MODE == kFusedCG) {
-                  if (rown) pap += static_cast<double>(val) * static_cast<double>(val);
+              if constexpr (MODE == kFusedCG) {
+                if (m & kOwnT) {
+                  pnl[st_goff[k]] = val;
+                  if (xupd) A.x[lnext + st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
                 }
               }
-              val = T(0);
+              if ((m & kBcYZ) || gxx == A.bcx_hi) {
+                if (m & kOwnT) {
+                  const bool rown = (m & kRownYZ) && gxx < A.ownx;
+                  yl[st_goff[k]] = rown ? val : T(0);
+                  if constexpr (MODE == kFusedCG) {
+                    if (rown) pap += static_cast<double>(val) * static_cast<double>(val);
+                  }
+                }
+                val = T(0);
+              }
+              v = val;
             }
-            v = val;
+            un[m >> 8] = v;
           }
-          un[m >> 8] = v;
+        }
+  #pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][e] = sX[NV + e];
+        }
+  #pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][NV + e] = pf_v[k];
         }
       }
-#pragma unroll
-      for (int k = 0; k < NPV; ++k) {
-        const int e = tid + k * NT;
-        if (e < NV) s_X[nxt][e] = sX[NV + e];
-      }
-#pragma unroll
-      for (int k = 0; k < NPV; ++k) {
-        const int e = tid + k * NT;
-        if (e < NV) s_X[nxt][NV + e] = pf_v[k];
-      }
+    };
+    // BDX_F3_STAGE_FIRST: consume the prefetch before the gather stores,
+    // behind one explicit vmcnt(0) (see BDX_F5_STAGE_FIRST)
+    if constexpr (BDX_F3_STAGE_FIRST) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      do_stage();
+      do_gather();
+    } else {
+      do_gather();
+      do_stage();
     }
+    kc_cur = kc_nxt;
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
