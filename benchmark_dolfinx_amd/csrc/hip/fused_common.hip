@@ -225,13 +225,17 @@ __global__ void __launch_bounds__(256)
     const V vy = *reinterpret_cast<const V*>(y + e0);
     V vr = *reinterpret_cast<const V*>(r + e0);
     bool any = false;
+    // (y, z) of the chunk's first element once; the others step along z
+    int ly = static_cast<int>(static_cast<float>(ein) * inv_tsz);
+    if (ly * tsz > ein) --ly;
+    if ((ly + 1) * tsz <= ein) ++ly;
+    int lz = ein - ly * tsz - 1;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
-      const int e = ein + w;
-      int ly = static_cast<int>(static_cast<float>(e) * inv_tsz);
-      if (ly * tsz > e) --ly;
-      if ((ly + 1) * tsz <= e) ++ly;
-      const int lz = e - ly * tsz;
+      if (++lz == tsz) {
+        lz = 0;
+        ++ly;
+      }
       const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz = static_cast<int64_t>(tZ) * tsz + lz;
       if (gy >= o1 || gz >= o2) continue;
       any = true;
