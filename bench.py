@@ -185,9 +185,14 @@ def run(comm, a) -> dict | None:
     if gpu and a.extras in ("on", "auto"):
         # the north-star variants of the same config (BASELINE.json: random
         # coefficients; the reference's --geom_perturb_fact general cells)
-        for key, kappa, pert in (("random_kappa", "random", a.perturb),
-                                 ("general", a.kappa, a.perturb or 0.1)):
-            extras[key] = _variant(comm, a, nx, degree, dtype, kappa, pert, sync, log)
+        # "general" takes the auto kernel (fused3's x-trilinear instance on
+        # these meshes); "general_trilinear" forces the fully general
+        # trilinear-geometry instance on the same mesh
+        for key, kappa, pert, geo in (("random_kappa", "random", a.perturb, a.geometry),
+                                      ("general", a.kappa, a.perturb or 0.1, a.geometry),
+                                      ("general_trilinear", a.kappa, a.perturb or 0.1,
+                                       "otf-general")):
+            extras[key] = _variant(comm, a, nx, degree, dtype, kappa, pert, sync, log, geo)
     if comm.rank != 0:
         return None
     return {
@@ -229,11 +234,12 @@ def run(comm, a) -> dict | None:
         },
         "random_kappa_gdofs": extras.get("random_kappa", {}).get("value"),
         "general_gdofs": extras.get("general", {}).get("value"),
+        "general_trilinear_gdofs": extras.get("general_trilinear", {}).get("value"),
         "variants": extras,
     }
 
 
-def _variant(comm, a, nx, degree, dtype, kappa, perturb, sync, log) -> dict:
+def _variant(comm, a, nx, degree, dtype, kappa, perturb, sync, log, geometry) -> dict:
     """Time one variant of the headline config (same mesh and degree) with
     its own operator and CG; min(steps, 50) timed iterations after 3 warmup."""
     import torch
@@ -245,7 +251,7 @@ def _variant(comm, a, nx, degree, dtype, kappa, perturb, sync, log) -> dict:
     pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, perturb, kappa)
     u = pb.assemble_rhs()
     x = pb.new_vector()
-    op = make_operator(pb, a.kernel, a.geometry)
+    op = make_operator(pb, a.kernel, geometry)
     steps = min(a.steps, 50)
     cg = DeviceCG(pb)
     cg.start(op, x, u)
@@ -261,7 +267,8 @@ def _variant(comm, a, nx, degree, dtype, kappa, perturb, sync, log) -> dict:
            "steps": steps, "kappa": kappa, "geom_perturb_fact": perturb,
            "kernel": getattr(op, "name", type(op).__name__),
            "geometry": getattr(op, "geometry", "otf"), "y_norm": pb.norm(x)}
-    log(f"variant kappa={kappa} perturb={perturb}: {rec['value']:.2f} GDoF/s ({rec['kernel']})")
+    log(f"variant kappa={kappa} perturb={perturb}: {rec['value']:.2f} GDoF/s "
+        f"({rec['kernel']}, {rec['geometry']})")
     if hasattr(op, "close"):
         op.close()
     del op, cg, x, u, pb

@@ -76,8 +76,14 @@ template <typename T, int NQ, int AFF> struct QUnroll3G {
 #ifndef BDX_FUSED3_GWAVES
 #define BDX_FUSED3_GWAVES 3
 #endif
+// AFF = 2 (x-trilinear cells, see the geometry block) carries ~10 geometry
+// registers instead of the 15-value trilinear set
+#ifndef BDX_FUSED3_XWAVES
+#define BDX_FUSED3_XWAVES 3
+#endif
 template <int NQ, int AFF> struct Fused3Waves {
-  static constexpr int value = AFF ? FusedWaves<NQ>::value : BDX_FUSED3_GWAVES;
+  static constexpr int value =
+      AFF == 1 ? FusedWaves<NQ>::value : (AFF == 2 ? BDX_FUSED3_XWAVES : BDX_FUSED3_GWAVES);
 };
 
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
@@ -342,6 +348,9 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
   T Js[3] = {0, 0, 0};                        // AFF = 0 only
   T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};
   T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};
+  // AFF = 2 only: 1/x_s, 1/hy, 1/hz, x_t/hy = bt0 + s bt1, x_u/hz = cu0 + s cu1,
+  // kappa w_t w_u det J / w_s
+  T xia = 0, xihy = 0, xihz = 0, xbt0 = 0, xbt1 = 0, xcu0 = 0, xcu1 = 0, xcs = 0;
 
   // per-cell coefficient: the next layer's value rides with the prefetch
   // batch (consumed in the same layer, its load made the waitcnt pass drain
@@ -478,7 +487,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
       const T* X1 = sX + NV;
       const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
       const int v10 = v00 + (TZ + 1) * 3;
-      if constexpr (AFF) {
+      if constexpr (AFF == 1) {
         T E[3], F[3], G[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -501,6 +510,32 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
         Gc[3] = sc * (K10 * K10 + K11 * K11 + K12 * K12);
         Gc[4] = sc * (K10 * K20 + K11 * K21 + K12 * K22);
         Gc[5] = sc * (K20 * K20 + K21 * K21 + K22 * K22);
+      } else if constexpr (AFF == 2) {
+        // x-trilinear cells: the vertex y (z) coordinates depend on the y (z)
+        // lattice index only (host-verified bitwise, models/poisson.py
+        // cells_x_trilinear), the class src/mesh.cpp:199-207's perturbation
+        // produces.  J = [[x_s, x_t, x_u], [0, hy, 0], [0, 0, hz]] with x_s
+        // constant along the thread's x column and x_t, x_u linear in s; the
+        // zero entries of the trilinear form below are dropped.
+        const T t = s_qw[a], uu = s_qw[b];
+        const int v11 = v10 + 3;
+        const T X000 = X0[v00], X001 = X0[v01], X010 = X0[v10], X011 = X0[v11];
+        const T X100 = X1[v00], X101 = X1[v01], X110 = X1[v10], X111 = X1[v11];
+        const T xs = (1 - t) * ((1 - uu) * (X100 - X000) + uu * (X101 - X001)) +
+                     t * ((1 - uu) * (X110 - X010) + uu * (X111 - X011));
+        const T xt0 = (1 - uu) * (X010 - X000) + uu * (X011 - X001);
+        const T xt1 = (1 - uu) * (X110 - X100) + uu * (X111 - X101) - xt0;
+        const T xu0 = (1 - t) * (X001 - X000) + t * (X011 - X010);
+        const T xu1 = (1 - t) * (X101 - X100) + t * (X111 - X110) - xu0;
+        const T hy = X0[v10 + 1] - X0[v00 + 1], hz = X0[v01 + 2] - X0[v00 + 2];
+        xia = fast_rcp(xs);
+        xihy = fast_rcp(hy);
+        xihz = fast_rcp(hz);
+        xbt0 = xt0 * xihy;
+        xbt1 = xt1 * xihy;
+        xcu0 = xu0 * xihz;
+        xcu1 = xu1 * xihz;
+        xcs = kwyz * xs * hy * hz;
       } else {
         const T t = s_qw[a], uu = s_qw[b];
         const int v11 = v10 + 3;
@@ -536,12 +571,24 @@ BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
         gzq += bq * tBD[i];
       }
       T fx, fy, fz;
-      if constexpr (AFF) {
+      if constexpr (AFF == 1) {
         const T w = s_qw[NQ + q];
         const T t0 = w * gxq, t1 = w * gyq, t2 = w * gzq;
         fx = Gc[0] * t0 + Gc[1] * t1 + Gc[2] * t2;
         fy = Gc[1] * t0 + Gc[3] * t1 + Gc[4] * t2;
         fz = Gc[2] * t0 + Gc[4] * t1 + Gc[5] * t2;
+      } else if constexpr (AFF == 2) {
+        // grad_X u = (p, gy/hy - bb p, gz/hz - cc p) with p = gx / x_s;
+        // F = kappa w det J^-1 grad_X u (16 operations per point)
+        const T s = s_qw[q];
+        const T bb = xbt0 + s * xbt1, cc = xcu0 + s * xcu1;
+        const T p = gxq * xia;
+        const T q1 = gyq * xihy - bb * p, q2 = gzq * xihz - cc * p;
+        const T sq = xcs * s_qw[NQ + q];
+        const T m0 = sq * p, m1 = sq * q1, m2 = sq * q2;
+        fy = m1 * xihy;
+        fz = m2 * xihz;
+        fx = (m0 - bb * m1 - cc * m2) * xia;
       } else {
         const T s = s_qw[q];
         const T J00 = Js[0], J10 = Js[1], J20 = Js[2];
@@ -828,8 +875,11 @@ int launch_fused3(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, 
   using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
-  if (affine)
+  // affine: 1 = parallelepipeds, 2 = x-trilinear (y/z lattice), 0 = trilinear
+  if (affine == 1)
     lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
+  else if (affine == 2)
+    lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 2><<<nblk, S::threads, 0, st>>>(a, tb);
   else
     lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 0><<<nblk, S::threads, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());
@@ -845,10 +895,12 @@ int fused3_resident(int affine) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
   const hipError_t e =
-      affine ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                   &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 1>, S::threads, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                   &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 0>, S::threads, 0);
+      affine == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 1>, S::threads, 0)
+      : affine == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                          &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 2>, S::threads, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                          &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 0>, S::threads, 0);
   return e == hipSuccess ? per_cu * cus : 0;
 }
 

@@ -78,8 +78,11 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
     if kernel == "fused3":
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 3) and geometry in ("auto", "otf", "otf-general"):
+            # "otf-general" forces the general trilinear instance; "auto" takes
+            # the x-trilinear one on the reference's perturbed meshes
             return FusedLaplacianGPU(pb, geometry="otf", version=3,
-                                     affine=geometry != "otf-general")
+                                     affine=geometry != "otf-general",
+                                     xtri=geometry != "otf-general")
         kernel = "fused2"
     if kernel == "fused2":
         from .models.fused import FusedLaplacianGPU, fused_supported

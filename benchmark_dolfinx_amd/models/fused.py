@@ -49,7 +49,7 @@ class FusedLaplacianGPU:
     parallelepiped cells, P = 3..7, FP64 / FP32)."""
 
     def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True,
-                 runtime: str = "native"):
+                 runtime: str = "native", xtri: bool | None = None):
         if geometry not in ("otf", "stored"):
             raise ValueError(f"unknown geometry mode {geometry}")
         if version >= 2 and geometry != "otf":
@@ -71,8 +71,17 @@ class FusedLaplacianGPU:
         self.affine_code = int(self.affine)
         if version == 5 and pb.all_axis_aligned:
             self.affine_code = 2
+        # fused3 takes 2 on x-trilinear meshes (y/z on the lattice, the
+        # reference's --geom_perturb_fact class): the 16-operation per-point
+        # geometry instead of the general trilinear one (BDX_F3_XTRI=0: off)
+        xtri = affine if xtri is None else xtri
+        self.x_trilinear = bool(version == 3 and xtri and not self.affine and pb.all_x_trilinear
+                                and os.environ.get("BDX_F3_XTRI", "1") != "0")
+        if self.x_trilinear:
+            self.affine_code = 2
         if version >= 2:
-            geometry = "otf-affine" if self.affine else "otf-general"
+            geometry = ("otf-affine" if self.affine else
+                        "otf-xtrilinear" if self.x_trilinear else "otf-general")
         self.name = "fused" if version == 1 else f"fused{version}"
         self.pb = pb
         self.geometry = geometry

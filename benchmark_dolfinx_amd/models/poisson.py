@@ -51,6 +51,20 @@ def cells_axis_aligned(X: np.ndarray) -> bool:
     return True
 
 
+def cells_x_trilinear(X: np.ndarray) -> bool:
+    """True iff the vertex y coordinates of the lattice X (nx+1, ny+1, nz+1, 3)
+    depend on the y index only and the z coordinates on the z index only
+    (bitwise), so every cell's Jacobian is [[x_s, x_t, x_u], [0, hy, 0],
+    [0, 0, hz]]: the class of `src/mesh.cpp:199-207`'s x-only perturbation.
+    Selects fused3's x-trilinear instance (AFF = 2)."""
+    for d, axes in ((1, (0, 2)), (2, (0, 1))):
+        for ax in axes:
+            E = np.diff(X[..., d], axis=ax)
+            if E.size and np.any(E != 0):
+                return False
+    return True
+
+
 def cells_all_parallelepipeds(X: np.ndarray) -> bool:
     """True iff every cell of the vertex lattice X (nx+1, ny+1, nz+1, 3) has
     bitwise-equal parallel edges (constant Jacobian).  Evaluated in the
@@ -116,6 +130,7 @@ class PoissonProblem:
         self.latd = self.lat.as_int64()
         self.all_affine = cells_all_parallelepipeds(self.xv_host)
         self.all_axis_aligned = self.all_affine and cells_axis_aligned(self.xv_host)
+        self.all_x_trilinear = cells_x_trilinear(self.xv_host)
         # per-cell kappa (None: the reference's constant kappa = 2)
         self.coefficient = coefficient
         kc = cell_coefficients(self.lat, coefficient, KAPPA)

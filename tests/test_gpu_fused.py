@@ -372,3 +372,54 @@ def test_fused_x_segments_partition_invariance(monkeypatch, version, pert, nseg,
     for r in got:
         for a, b in zip(r, ref):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
+
+
+@pytest.mark.parametrize("nc,P,dt", [((4, 5, 7), 3, torch.float64), ((3, 7, 11), 3, torch.float64),
+                                     ((2, 3, 3), 6, torch.float64), ((3, 3, 8), 5, torch.float64),
+                                     ((5, 4, 7), 3, torch.float32), ((2, 3, 3), 6, torch.float32),
+                                     ((3, 4, 9), 4, torch.float64), ((7, 9, 13), 1, torch.float64),
+                                     ((2, 3, 4), 7, torch.float64)])
+@pytest.mark.parametrize("coef", ["constant", "random"])
+def test_fused3_x_trilinear_instance(nc, P, dt, coef):
+    """fused3's x-trilinear instance (AFF = 2: y/z on the lattice, x perturbed
+    as src/mesh.cpp:199-207) is auto-selected on perturbed meshes and matches
+    the CPU operator and the general trilinear instance; a sheared perturbed
+    mesh keeps the general instance."""
+    from benchmark_dolfinx_amd.driver import make_operator
+    gpu = PoissonProblem(Comm(), nc, P, 1, False, dt, "gpu", 0.2, coef)
+    _skip_unsupported(gpu, 3)
+    cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", 0.2, coef)
+    op = make_operator(gpu)
+    assert op.name == "fused3" and op.geometry == "otf-xtrilinear" and op.affine_code == 2
+    gen = make_operator(gpu, "fused3", "otf-general")
+    assert gen.geometry == "otf-general" and gen.affine_code == 0
+    rng = np.random.default_rng(11)
+    u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
+    yc = cpu.new_vector()
+    MatFreeLaplacianCPU(cpu).apply(u64, yc)
+    o = cpu.owned
+    scale = max(1.0, yc.abs().max().item())
+    for k in (op, gen):
+        yg = torch.full(gpu.lat.shape, float("nan"), dtype=dt, device=gpu.device)
+        k.apply(u64.to(gpu.device, dt), yg)
+        yg = yg.double().cpu()
+        assert torch.isfinite(o(yg)).all()
+        err = (o(yg) - o(yc)).abs().max().item()
+        assert err <= _tol(dt) * 50 * scale, (k.geometry, err)
+    if dt == torch.float64:
+        xg = gpu.new_vector()
+        DeviceCG(gpu).solve(op, xg, gpu.assemble_rhs(), 12)
+        xc = cpu.new_vector()
+        cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 12)
+        rel = (o(xg.cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
+        assert rel < 1e-10, rel
+    sh = PoissonProblem(Comm(), nc, P, 1, False, dt, "gpu", 0.2, coef, 0.3)
+    assert make_operator(sh).geometry == "otf-general"
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_fused3_x_trilinear_partition_invariance(ranks):
+    ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", 3, 0.15)[0]
+    for r in run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf", 3, 0.15):
+        for a, b in zip(r, ref):
+            assert abs(a - b) <= 1e-11 * abs(b), (r, ref)

@@ -157,3 +157,23 @@ def test_sheared_mesh_is_parallelepiped_with_full_jacobian():
     J = np.stack([X[1, 0, 0] - X[0, 0, 0], X[0, 1, 0] - X[0, 0, 0], X[0, 0, 1] - X[0, 0, 0]], 1)
     off = J - np.diag(np.diag(J))
     assert np.all(np.abs(off[np.nonzero(off)]) > 0) and np.count_nonzero(off) == 3
+
+
+def test_x_trilinear_classification():
+    """The reference's --geom_perturb_fact moves vertex x only
+    (src/mesh.cpp:199-207): such meshes are x-trilinear (fused3 AFF = 2);
+    sheared meshes are not, boxes are."""
+    import torch
+
+    from benchmark_dolfinx_amd.models.poisson import PoissonProblem, cells_x_trilinear
+    from benchmark_dolfinx_amd.parallel.comm import Comm
+    box = PoissonProblem(Comm(), (3, 4, 5), 2, 1, False, torch.float64, "cpu")
+    pert = PoissonProblem(Comm(), (3, 4, 5), 2, 1, False, torch.float64, "cpu", 0.2)
+    shear = PoissonProblem(Comm(), (3, 4, 5), 2, 1, False, torch.float64, "cpu", 0.2,
+                           "constant", 0.3)
+    assert box.all_x_trilinear and box.all_affine
+    assert pert.all_x_trilinear and not pert.all_affine
+    assert not shear.all_x_trilinear
+    X = pert.xv_host.copy()
+    X[1, 2, 3, 1] += 1e-3  # one y coordinate off the lattice
+    assert not cells_x_trilinear(X)
