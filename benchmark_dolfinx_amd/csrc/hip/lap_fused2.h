@@ -327,6 +327,9 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
   T Js[3] = {0, 0, 0};                        // AFF = 0 only
   T Jt0[3] = {0, 0, 0}, Jt1[3] = {0, 0, 0};
   T Ju0[3] = {0, 0, 0}, Ju1[3] = {0, 0, 0};
+  // AFF = 2 only (x-trilinear cells, see lap_fused3.h): 1/x_s, 1/hy, 1/hz,
+  // x_t/hy = bt0 + s bt1, x_u/hz = cu0 + s cu1, kappa w_t w_u det J / w_s
+  T xia = 0, xihy = 0, xihz = 0, xbt0 = 0, xbt1 = 0, xcu0 = 0, xcu1 = 0, xcs = 0;
 
   for (int cx = cbeg; cx < cend; ++cx) {
     const int cur = (cx - cbeg) & 1, nxt = cur ^ 1;
@@ -461,7 +464,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
       const T* X1 = sX + NV;
       const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
       const int v10 = v00 + (TZ + 1) * 3;
-      if constexpr (AFF) {
+      if constexpr (AFF == 1) {
         T E[3], F[3], G[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -484,6 +487,27 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
         Gc[3] = sc * (K10 * K10 + K11 * K11 + K12 * K12);
         Gc[4] = sc * (K10 * K20 + K11 * K21 + K12 * K22);
         Gc[5] = sc * (K20 * K20 + K21 * K21 + K22 * K22);
+      } else if constexpr (AFF == 2) {
+        // x-trilinear cells (y/z on the lattice; lap_fused3.h AFF = 2)
+        const T t = s_qw[a], uu = s_qw[b];
+        const int v11 = v10 + 3;
+        const T X000 = X0[v00], X001 = X0[v01], X010 = X0[v10], X011 = X0[v11];
+        const T X100 = X1[v00], X101 = X1[v01], X110 = X1[v10], X111 = X1[v11];
+        const T xs = (1 - t) * ((1 - uu) * (X100 - X000) + uu * (X101 - X001)) +
+                     t * ((1 - uu) * (X110 - X010) + uu * (X111 - X011));
+        const T xt0 = (1 - uu) * (X010 - X000) + uu * (X011 - X001);
+        const T xt1 = (1 - uu) * (X110 - X100) + uu * (X111 - X101) - xt0;
+        const T xu0 = (1 - t) * (X001 - X000) + t * (X011 - X010);
+        const T xu1 = (1 - t) * (X101 - X100) + t * (X111 - X110) - xu0;
+        const T hy = X0[v10 + 1] - X0[v00 + 1], hz = X0[v01 + 2] - X0[v00 + 2];
+        xia = fast_rcp(xs);
+        xihy = fast_rcp(hy);
+        xihz = fast_rcp(hz);
+        xbt0 = xt0 * xihy;
+        xbt1 = xt1 * xihy;
+        xcu0 = xu0 * xihz;
+        xcu1 = xu1 * xihz;
+        xcs = kwyz * xs * hy * hz;
       } else {
         const T t = s_qw[a], uu = s_qw[b];
         const int v11 = v10 + 3;
@@ -522,13 +546,24 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
         }
       }
     };
-    if constexpr (AFF) {
+    if constexpr (AFF == 1) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const T w = s_qw[NQ + q];
         const T t0 = w * gx[q], t1 = w * gy[q], t2 = w * gz[q];
         emit(q, Gc[0] * t0 + Gc[1] * t1 + Gc[2] * t2, Gc[1] * t0 + Gc[3] * t1 + Gc[4] * t2,
              Gc[2] * t0 + Gc[4] * t1 + Gc[5] * t2);
+      }
+    } else if constexpr (AFF == 2) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const T s = s_qw[q];
+        const T bb = xbt0 + s * xbt1, cc = xcu0 + s * xcu1;
+        const T p = gx[q] * xia;
+        const T q1 = gy[q] * xihy - bb * p, q2 = gz[q] * xihz - cc * p;
+        const T sq = xcs * s_qw[NQ + q];
+        const T m0 = sq * p, m1 = sq * q1, m2 = sq * q2;
+        emit(q, (m0 - bb * m1 - cc * m2) * xia, m1 * xihy, m2 * xihz);
       }
     } else {
 #pragma unroll
@@ -748,8 +783,11 @@ int launch_fused2(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, 
   using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
-  if (affine)
+  // affine: 1 = parallelepipeds, 2 = x-trilinear (y/z lattice), 0 = trilinear
+  if (affine == 1)
     lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
+  else if (affine == 2)
+    lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 2><<<nblk, S::threads, 0, st>>>(a, tb);
   else
     lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 0><<<nblk, S::threads, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());
@@ -765,10 +803,12 @@ int fused2_resident(int affine) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
   const hipError_t e =
-      affine ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                   &per_cu, lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 1>, S::threads, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                   &per_cu, lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 0>, S::threads, 0);
+      affine == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &per_cu, lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 1>, S::threads, 0)
+      : affine == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                          &per_cu, lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 2>, S::threads, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                          &per_cu, lap_fused2_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 0>, S::threads, 0);
   return e == hipSuccess ? per_cu * cus : 0;
 }
 

@@ -88,7 +88,8 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 2) and geometry in ("auto", "otf", "otf-general"):
             return FusedLaplacianGPU(pb, geometry="otf", version=2,
-                                     affine=geometry != "otf-general")
+                                     affine=geometry != "otf-general",
+                                     xtri=geometry != "otf-general")
         kernel = "fused"
     if geometry == "otf-general":
         geometry = "otf"

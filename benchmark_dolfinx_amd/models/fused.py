@@ -71,11 +71,11 @@ class FusedLaplacianGPU:
         self.affine_code = int(self.affine)
         if version == 5 and pb.all_axis_aligned:
             self.affine_code = 2
-        # fused3 takes 2 on x-trilinear meshes (y/z on the lattice, the
+        # fused2/3 take 2 on x-trilinear meshes (y/z on the lattice, the
         # reference's --geom_perturb_fact class): the 16-operation per-point
         # geometry instead of the general trilinear one (BDX_F3_XTRI=0: off)
         xtri = affine if xtri is None else xtri
-        self.x_trilinear = bool(version == 3 and xtri and not self.affine and pb.all_x_trilinear
+        self.x_trilinear = bool(version in (2, 3) and xtri and not self.affine and pb.all_x_trilinear
                                 and os.environ.get("BDX_F3_XTRI", "1") != "0")
         if self.x_trilinear:
             self.affine_code = 2

@@ -423,3 +423,30 @@ def test_fused3_x_trilinear_partition_invariance(ranks):
     for r in run_threaded(ranks, _cg_job, (6, 7, 9), 3, 15, "otf", 3, 0.15):
         for a, b in zip(r, ref):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
+
+
+@pytest.mark.parametrize("nc,P,qm,g,dt", [((4, 5, 7), 3, 0, False, torch.float64),
+                                         ((2, 3, 3), 6, 0, False, torch.float64),
+                                         ((5, 4, 7), 3, 0, False, torch.float32),
+                                         ((3, 7, 11), 2, 1, True, torch.float64)])
+def test_fused2_x_trilinear_instance(nc, P, qm, g, dt):
+    """fused2's x-trilinear instance (qmode=0 GLL collocation, or forced)
+    against the CPU operator and fused2's general instance."""
+    gpu = PoissonProblem(Comm(), nc, P, qm, g, dt, "gpu", 0.2)
+    _skip_unsupported(gpu, 2)
+    cpu = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "cpu", 0.2)
+    xt = FusedLaplacianGPU(gpu, "otf", 2)
+    gen = FusedLaplacianGPU(gpu, "otf", 2, affine=False)
+    assert xt.affine_code == 2 and xt.geometry == "otf-xtrilinear" and gen.affine_code == 0
+    rng = np.random.default_rng(12)
+    u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
+    yc = cpu.new_vector()
+    MatFreeLaplacianCPU(cpu).apply(u64, yc)
+    o = cpu.owned
+    scale = max(1.0, yc.abs().max().item())
+    for k in (xt, gen):
+        yg = torch.full(gpu.lat.shape, float("nan"), dtype=dt, device=gpu.device)
+        k.apply(u64.to(gpu.device, dt), yg)
+        yg = yg.double().cpu()
+        err = (o(yg) - o(yc)).abs().max().item()
+        assert err <= _tol(dt) * 50 * scale, (k.geometry, err)
