@@ -62,14 +62,16 @@ template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 
 // general-geometry instances: BDX_F3_GQUNROLL > 0 overrides the x-loop unroll
 // (rolled: the per-point geometry of one point at a time is live, not NQ)
 // (FP32 at NQ > 5 keeps the 2-way unroll: 34.4 vs 33.9 GDoF/s at Q6)
-// x-trilinear instances (AFF = 2): BDX_F3_XQUNROLL > 0 overrides the unroll
+// x-trilinear FP64 instances (AFF = 2): BDX_F3_XQUNROLL > 0 overrides the
+// unroll.  Rolled (1) measured Q3 25.0 -> 26.2 GDoF/s, Q6 neutral (29.0 both);
+// FP32 keeps the default (Q6 46.2 vs 46.1 rolled), profiles/r2_xtrilinear.md
 #ifndef BDX_F3_XQUNROLL
-#define BDX_F3_XQUNROLL 0
+#define BDX_F3_XQUNROLL 1
 #endif
 template <typename T, int NQ, int AFF> struct QUnroll3G {
   static constexpr bool on = !AFF && BDX_F3_GQUNROLL > 0 && (sizeof(T) == 8 || NQ <= 5);
   static constexpr int value = on ? BDX_F3_GQUNROLL
-                               : (AFF == 2 && BDX_F3_XQUNROLL > 0) ? BDX_F3_XQUNROLL
+                               : (AFF == 2 && BDX_F3_XQUNROLL > 0 && sizeof(T) == 8) ? BDX_F3_XQUNROLL
                                                                    : QUnroll3<NQ>::value;
 };
 // Waves per SIMD the general (trilinear, AFF = 0) instances are compiled for.
