@@ -170,7 +170,8 @@ def run(comm, a) -> dict | None:
     if rt is not None and a.profile_steps > 0:
         phases = rt.profile(a.profile_steps)
         allp = comm.gather_objects(phases)
-        phases_max = {k: max(p[k] for p in allp) for k in phases}
+        phases_max = {k: (all(p[k] for p in allp) if isinstance(phases[k], bool)
+                          else max(p[k] for p in allp)) for k in phases}
     if hasattr(op, "close"):
         op.close()
     px, py, pz = pb.lat.pgrid

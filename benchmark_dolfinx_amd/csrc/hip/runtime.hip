@@ -666,6 +666,12 @@ struct CGRuntime {
       out[6] += dt(kMPap, kMUpd);
       out[7] += dt(kMUpd, kMEnd);
       out[8] += dt(kMStart, kMEnd);
+      // timeline offsets from the iteration start: an exchange is hidden when
+      // it completes before the compute-stream work it overlaps does
+      out[9] += dt(kMStart, kMFwdEnd);
+      out[10] += dt(kMStart, kMOpA);
+      out[11] += dt(kMStart, kMRevEnd);
+      out[12] += dt(kMStart, kMOpB);
     }
     prof = false;
     if (!rc) rc = flush();
@@ -674,7 +680,7 @@ struct CGRuntime {
     for (int i = 0; i < kNPhases && n > 0; ++i) out[i] /= static_cast<double>(n);
     return rc;
   }
-  static constexpr int kNPhases = 9;
+  static constexpr int kNPhases = 13;
 
   ~CGRuntime() {
     drop_graphs();
@@ -970,7 +976,7 @@ int bdx_rt_wait(void* h) {
   return with_rt(h, [](auto* rt) { return rt->tr->wait(rt->ev_out); });
 }
 
-// n eager CG iterations with hipEvent phase timers; out (9 doubles, mean ms):
+// n eager CG iterations with hipEvent phase timers; out (13 doubles, mean ms):
 //   0 forward halo (comm stream: pack, exchange, unpack)
 //   1 operator, interior tiles A (serial schedule: the whole operator)
 //   2 ghost-touching tiles + ghost finalize (waits for the forward halo)
@@ -980,6 +986,8 @@ int bdx_rt_wait(void* h) {
 //   6 r update + r.r
 //   7 all-reduce(r.r)
 //   8 whole iteration
+//   9..12 end of the forward halo / interior tiles A / reverse halo / interior
+//         tiles B, measured from the iteration start (overlap evidence)
 int bdx_rt_profile(void* h, long n, double* out, int nout) {
   return with_rt(h, [&](auto* rt) { return rt->profile(n, out, nout); });
 }

@@ -28,7 +28,11 @@ from ..ops.native import ptr
 
 
 PHASES = ("halo_fwd", "op_interior_a", "op_boundary", "halo_rev", "op_interior_b",
-          "reduce_allreduce_pap", "update_rr", "allreduce_rr", "iteration")
+          "reduce_allreduce_pap", "update_rr", "allreduce_rr", "iteration",
+          # offsets from the iteration start (the exchange is hidden when its
+          # end precedes the end of the interior tiles it overlaps)
+          "t_halo_fwd_done", "t_op_interior_a_done", "t_halo_rev_done",
+          "t_op_interior_b_done")
 
 
 def _agree(comm, ok: bool) -> bool:
@@ -186,7 +190,10 @@ class NativeCGRuntime:
         out = (ctypes.c_double * len(PHASES))()
         _check(self.lib.bdx_rt_profile(self.h, int(n), out, len(PHASES)), "rt_profile")
         self._sync_state()
-        return {k: float(v) for k, v in zip(PHASES, out)}
+        ph = {k: float(v) for k, v in zip(PHASES, out)}
+        ph["halo_fwd_hidden"] = ph["t_halo_fwd_done"] <= ph["t_op_interior_a_done"]
+        ph["halo_rev_hidden"] = ph["t_halo_rev_done"] <= ph["t_op_interior_b_done"]
+        return ph
 
     def close(self) -> None:
         if getattr(self, "h", None):

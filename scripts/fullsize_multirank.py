@@ -52,6 +52,7 @@ def main():
                           "partition": out["config"]["parallelism"],
                           "runtime": out["config"]["runtime"],
                           "y_norm": out["config"]["y_norm"],
+                          "phases_ms_max_over_ranks": out["config"]["phases_ms_max_over_ranks"],
                           "wall_s": round(time.perf_counter() - t0, 1)}), flush=True)
     y1, yn = res[a.ref_ranks]["config"]["y_norm"], res[a.ranks]["config"]["y_norm"]
     rel = abs(y1 - yn) / abs(y1)

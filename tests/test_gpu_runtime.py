@@ -158,6 +158,10 @@ def test_phase_profile_single_and_threaded():
             assert it == 7
             assert ph["iteration"] > 0 and ph["op_interior_a"] > 0
             assert all(v >= 0 for v in ph.values())
+            assert isinstance(ph["halo_fwd_hidden"], bool)
+            for k in ("t_halo_fwd_done", "t_op_interior_a_done", "t_halo_rev_done",
+                      "t_op_interior_b_done"):
+                assert ph[k] <= ph["iteration"] + 1e-3, (k, ph)
             if ranks > 1:
                 assert ph["halo_fwd"] > 0 and ph["halo_rev"] > 0
 
