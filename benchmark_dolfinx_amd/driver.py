@@ -45,7 +45,9 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
             # general (trilinear) cells, same-box A/B (scripts/job_r2i.sh,
             # job_r2r.sh): Q3 fused3 18.2 vs fused2 16.5 GDoF/s; Q6 fused3
             # 22.0 (spill-free) vs fused2 18.8; fused3 falls back to fused2
-            # where it does not apply (phi0 = I)
+            # where it does not apply (phi0 = I).  On the reference's
+            # x-perturbed meshes both take their x-trilinear instance
+            # (profiles/r2_xtrilinear.md: Q3 26.2, Q6 29.1 GDoF/s)
             kernel = "fused3"
         else:
             # Kronecker cores on parallelepiped meshes.  fused5 (nodal sum
