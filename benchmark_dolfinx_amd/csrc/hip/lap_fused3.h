@@ -55,6 +55,10 @@
 #ifndef BDX_F3_ORECOMP
 #define BDX_F3_ORECOMP 1
 #endif
+// x-trilinear instances recompute the output descriptors as well (A/B switch)
+#ifndef BDX_F3_XORECOMP
+#define BDX_F3_XORECOMP 0
+#endif
 #ifndef BDX_F3_GQUNROLL
 #define BDX_F3_GQUNROLL 1
 #endif
@@ -298,7 +302,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
   // (frees 4 NOUT VGPRs: the Q6 general CG instance spilled 34 dwords with them
   // resident; same-box Q6 general 18.8 -> 22.0 GDoF/s, while Q3 general, which
   // did not spill, drops 18.2 -> 14.0 with the recomputation)
-  constexpr bool ORECOMP = BDX_F3_ORECOMP && !AFF && NQ >= 7;
+  constexpr bool ORECOMP = BDX_F3_ORECOMP && (AFF == 0 || (AFF == 2 && BDX_F3_XORECOMP)) && NQ >= 7;
   int o_src[ORECOMP ? 1 : NOUT][2], o_off[ORECOMP ? 1 : NOUT], o_meta[ORECOMP ? 1 : NOUT];
   if constexpr (!ORECOMP) {
 #pragma unroll
