@@ -960,7 +960,10 @@ int fused3_resident(int affine) {
   }                                                                                \
   extern "C" int bdx_fused3_segments_##SUF##_p##PP(int affine_ok, int nq, int tiles, int ncx) { \
     if (nq != PP + 2) return 1;                                                    \
-    return fused_choose_segments(tiles, ncx, fused3_resident<T, PP + 1, PP + 2>(affine_ok)); \
+    const int s = fused_choose_segments(tiles, ncx, fused3_resident<T, PP + 1, PP + 2>(affine_ok)); \
+    /* x-trilinear: at least 2 segments (measured 1 -> 2: Q3 +1.5 %, Q6 +3.7 %, \
+       Q6 FP32 +4.0 %, profiles/r2_xtrilinear.md) */                              \
+    return (affine_ok == 2 && s < 2 && ncx >= 8) ? 2 : s;                           \
   }
 
 // Packed tables of the fused3 core (layout: OFF_BR/OFF_DR rows of B = phi0 and
