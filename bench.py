@@ -178,6 +178,7 @@ def run(comm, a) -> dict | None:
     mesh_nx, ndofs_global = list(nx), pb.ndofs_global
     kname = getattr(op, "name", type(op).__name__)
     geom = getattr(op, "geometry", "otf")
+    xseg = getattr(op, "nseg", None)
     del op, x, u, pb, rt
     if gpu:
         del cg
@@ -220,6 +221,7 @@ def run(comm, a) -> dict | None:
             "mesh": mesh_nx,
             "kernel": kname,
             "geometry": geom,
+            "x_segments": xseg,
             "kappa": a.kappa,
             "geom_perturb_fact": a.perturb,
             "runtime": runtime,
