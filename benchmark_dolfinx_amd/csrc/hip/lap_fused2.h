@@ -907,8 +907,13 @@ inline int fused_choose_segments(int tiles, int ncx, int resident) {
   for (int S = 1; S <= 16 && S <= ncx; ++S) {
     const int len = (ncx + S - 1) / S;
     const int segs = (ncx + len - 1) / len;
-    const double rounds = static_cast<double>((static_cast<int64_t>(tiles) * segs + resident - 1) /
-                                              resident);
+    // fractional rounds plus half a round of tail: workgroups do not run in
+    // lock-step rounds, so a launch of 17.02 rounds costs about 17.5, not 18
+    // (whole-round model vs this one, same box: fused5 Q3 6 -> 3 segments
+    // 61.0 -> 61.7 GDoF/s, Q6 1 -> 2 segments 53.5 -> 54.3, fused3
+    // x-trilinear Q6 1 -> 2 28.8 -> 29.8; profiles/r2_segments.md)
+    const double rounds =
+        static_cast<double>(static_cast<int64_t>(tiles) * segs) / resident + 0.5;
     // per work item: its layers, the redundant layer, and ~1 layer of
     // unpipelined prologue
     const double cost = rounds * (len + (S > 1 ? 2.0 : 1.0));
