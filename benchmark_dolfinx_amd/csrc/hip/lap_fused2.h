@@ -900,6 +900,9 @@ inline int fused_set_rect(Fused2Args<T>& a, const int* rect) {
 // synchronisation, bitwise identical to S = 1 except for the order of the
 // p.Ap partial sums (one per work item).
 //   mode argument of the apply entry points: kind | (S << 8), S = 0 -> 1.
+#ifndef BDX_SEG_WHOLE_ROUNDS
+#define BDX_SEG_WHOLE_ROUNDS 0  // A/B switch: the round-1 whole-round model
+#endif
 inline int fused_choose_segments(int tiles, int ncx, int resident) {
   if (tiles <= 0 || ncx <= 1 || resident <= 0) return 1;
   int best = 1;
@@ -912,8 +915,13 @@ inline int fused_choose_segments(int tiles, int ncx, int resident) {
     // (whole-round model vs this one, same box: fused5 Q3 6 -> 3 segments
     // 61.0 -> 61.7 GDoF/s, Q6 1 -> 2 segments 53.5 -> 54.3, fused3
     // x-trilinear Q6 1 -> 2 28.8 -> 29.8; profiles/r2_segments.md)
+#if BDX_SEG_WHOLE_ROUNDS
+    const double rounds = static_cast<double>((static_cast<int64_t>(tiles) * segs + resident - 1) /
+                                              resident);
+#else
     const double rounds =
         static_cast<double>(static_cast<int64_t>(tiles) * segs) / resident + 0.5;
+#endif
     // per work item: its layers, the redundant layer, and ~1 layer of
     // unpipelined prologue
     const double cost = rounds * (len + (S > 1 ? 2.0 : 1.0));
