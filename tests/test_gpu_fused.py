@@ -450,3 +450,18 @@ def test_fused2_x_trilinear_instance(nc, P, qm, g, dt):
         yg = yg.double().cpu()
         err = (o(yg) - o(yc)).abs().max().item()
         assert err <= _tol(dt) * 50 * scale, (k.geometry, err)
+
+
+def test_segment_model_choices():
+    """The fractional-round segment model (lap_fused2.h fused_choose_segments)
+    on the headline tile counts: fused5 Q6 (66 x 66 tiles, 132 layers) splits
+    the march (whole rounds kept S = 1), fused3's x-trilinear instance takes at
+    least 2 segments, and no choice exceeds the layer count (profiles/r2_segments.md)."""
+    from benchmark_dolfinx_amd.ops import native
+    lib = native.hip()
+    assert lib.bdx_fused5_segments_f64_p6(2, 66 * 66, 132) >= 2
+    assert lib.bdx_fused3_segments_f64_p6(2, 8, 66 * 66, 132) >= 2
+    assert 1 <= lib.bdx_fused3_segments_f64_p3(2, 5, 2, 4) <= 4
+    for s in (lib.bdx_fused5_segments_f64_p3(2, 56 * 56, 222),
+              lib.bdx_fused3_segments_f64_p3(0, 5, 112 * 45, 222)):
+        assert 1 <= s <= 16
