@@ -63,17 +63,29 @@ def parse_args(argv=None):
                          "the config's DoF target")
     ap.add_argument("--profile-steps", type=int, default=5,
                     help="extra eager iterations with hipEvent phase timers (0: none)")
+    ap.add_argument("--companions", default="auto", choices=["auto", "on", "off"],
+                    help="after the Q3 headline, time the metric's second half (Q6 at 500 M "
+                         "DoFs/GPU, FP64 and FP32) with the same steps/warmup and report "
+                         "q6_gdofs / q6f32_gdofs (auto: on for the q3 config)")
     ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
-                    help="after the headline run, time the same config with per-cell random "
-                         "coefficients and on the perturbed (general trilinear) mesh and report "
-                         "random_kappa_gdofs / general_gdofs (GPU platform only)")
+                    help="after the headline, time variants of it: per-cell random "
+                         "coefficients, the perturbed (general trilinear) mesh, the "
+                         "reference's data model (dofmap + stored G) and Q6 perturbed "
+                         "(GPU only; auto: on for one rank)")
     return ap.parse_args(argv)
 
 
-def run(comm, a) -> dict | None:
-    """The timed CG benchmark on an initialised communicator; returns rank 0's
-    JSON record (None elsewhere).  Callable in-process (tests run it on
-    threaded ranks with RCCL semantics emulated)."""
+def _median(v):
+    s = sorted(v)
+    n = len(s)
+    return None if n == 0 else (s[n // 2] if n % 2 else 0.5 * (s[n // 2 - 1] + s[n // 2]))
+
+
+def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
+             kernel="auto", geometry="auto", profile_steps=0, log=None) -> dict:
+    """Build one config, run `warmup` untimed and `steps` timed CG
+    iterations (barrier + device sync on both sides, MAX over ranks) and
+    return its record (identical on every rank)."""
     import torch
 
     from benchmark_dolfinx_amd.driver import make_operator
@@ -81,9 +93,139 @@ def run(comm, a) -> dict | None:
     from benchmark_dolfinx_amd.models.poisson import PoissonProblem
     from benchmark_dolfinx_amd.solvers.cg import DeviceCG, cg_solve
 
-    degree, dpg, bits, base = CONFIGS[a.config]
+    degree, dpg, bits, base = CONFIGS[config]
     if a.dofs_per_gpu:
         dpg = a.dofs_per_gpu
+    n = comm.size
+    gpu = a.platform == "gpu"
+    dtype = torch.float64 if bits == 64 else torch.float32
+    nx = (tuple(int(v) for v in a.mesh.split(",")) if a.mesh
+          else compute_mesh_size(dpg * n, degree))
+    log = log or (lambda msg: None)
+
+    t_setup = time.perf_counter()
+    phase_t = {}
+
+    def mark(name):
+        phase_t[name] = time.perf_counter() - t_setup - sum(phase_t.values())
+
+    log(f"{config}: mesh {nx} degree {degree} fp{bits} on {n} rank(s), kappa={kappa} "
+        f"perturb={perturb} kernel={kernel} geometry={geometry}")
+    pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, perturb, kappa)
+    mark("problem")
+    u = pb.assemble_rhs()
+    x = pb.new_vector()
+    mark("rhs")
+    op = make_operator(pb, kernel, geometry)
+    mark("operator")
+
+    def sync():
+        if gpu:
+            torch.cuda.synchronize()
+        comm.barrier()
+        if gpu:
+            torch.cuda.synchronize()
+
+    cg = None
+    if gpu:
+        cg = DeviceCG(pb)
+        cg.start(op, x, u)
+        cg.iterate(warmup)
+        cg.wait()
+    else:
+        cg_solve(op, pb, x, u, warmup, 0.0)
+    sync()
+    mark("warmup")
+    t_setup = time.perf_counter() - t_setup
+    t0 = time.perf_counter()
+    step_ms = []
+    if gpu:
+        step_ms = cg.iterate_timed(steps)
+        cg.wait()  # bounded by the RCCL deadline: a hung peer raises
+    else:
+        cg_solve(op, pb, x, u, steps, 0.0)
+    sync()
+    dt = time.perf_counter() - t0
+    rank_dt = comm.gather_objects(dt)
+    dt = comm.allreduce_scalar(dt, "max")
+    value = pb.ndofs_global * steps / (1e9 * dt)
+    med = _median(step_ms)
+    med = comm.allreduce_scalar(med, "max") if med is not None else None
+    smin = comm.allreduce_scalar(min(step_ms), "max") if step_ms else None
+    ynorm = pb.norm(x)
+    rt = getattr(op, "_rt", None)
+    rec = {
+        "value": value,
+        "ms_per_step": 1e3 * dt / steps,
+        "ms_per_step_median": med,
+        "ms_per_step_min": smin,
+        "steps": steps,
+        "warmup": warmup,
+        "vs_baseline": (value / (base * n)) if base else None,
+        "dtype": "fp64" if bits == 64 else "fp32",
+        "degree": degree,
+        "dofs_per_gpu": dpg,
+        "ndofs_global": pb.ndofs_global,
+        "mesh": list(nx),
+        "partition": list(pb.lat.pgrid),
+        "kernel": getattr(op, "name", type(op).__name__),
+        "geometry": getattr(op, "geometry", "otf"),
+        "x_segments": getattr(op, "nseg", None),
+        "kappa": kappa,
+        "geom_perturb_fact": perturb,
+        "y_norm": ynorm,
+        "setup_s": t_setup,
+        "setup_phases_s": phase_t,
+        "runtime": (f"native C++ ({rt.transport}, hipGraph={rt.graphs}, overlap={rt.overlap}, "
+                    f"tiled={rt.tiled})" if rt is not None else "python"),
+        "comm": {"torch_backend": comm.backend, "torch_world": comm.size,
+                 "transport": rt.transport if rt is not None else "python",
+                 "rccl_ranks": rt.comm_ranks() if rt is not None else None,
+                 "graphs": rt.graphs if rt is not None else False,
+                 "halo_overlap": rt.overlap if rt is not None else False,
+                 "halo_bytes_per_exchange": pb.halo.bytes_per_exchange,
+                 "rank_ms_per_step_max": 1e3 * max(rank_dt) / steps,
+                 "rank_ms_per_step_min": 1e3 * min(rank_dt) / steps},
+    }
+    # phase attribution: a few extra eager iterations with hipEvent timers,
+    # after the timed loop and the norm (outside the measurement)
+    if rt is not None and profile_steps > 0:
+        phases = rt.profile(profile_steps)
+        allp = comm.gather_objects(phases)
+        rec["phases_ms"] = phases
+        rec["phases_ms_max_over_ranks"] = {
+            k: (all(p[k] for p in allp) if isinstance(phases[k], bool)
+                else max(p[k] for p in allp)) for k in phases}
+    log(f"{config}: {value:.2f} GDoF/s ({rec['ms_per_step']:.3f} ms/step, median "
+        f"{med if med is None else round(med, 3)} ms; {rec['kernel']}, {rec['geometry']})")
+    if hasattr(op, "close"):
+        op.close()
+    del op, x, u, pb, rt, cg
+    if gpu:
+        torch.cuda.empty_cache()
+    return rec
+
+
+def _guarded(comm, fn, log) -> dict:
+    """Run one secondary measurement; an error is recorded, not raised, so
+    the already measured headline is always reported."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 - reported in the JSON
+        log(f"secondary measurement failed: {e!r}")
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.empty_cache()
+        except Exception:  # noqa: BLE001
+            pass
+        return {"value": None, "error": repr(e)}
+
+
+def run(comm, a) -> dict | None:
+    """The timed CG benchmark on an initialised communicator; returns rank 0's
+    JSON record (None elsewhere).  Callable in-process (tests run it on
+    threaded ranks with RCCL semantics emulated)."""
     n = comm.size
     gpu = a.platform == "gpu"
     flags = None
@@ -94,10 +236,6 @@ def run(comm, a) -> dict | None:
             raise SystemExit(f"bench.py: the HIP library was built with timing-only phase "
                              f"drops {flags['drops']} (wrong numerics); refusing to time it "
                              f"(BDX_ALLOW_DROP=1 runs it, marked invalid)")
-    dtype = torch.float64 if bits == 64 else torch.float32
-    nx = (tuple(int(v) for v in a.mesh.split(",")) if a.mesh
-          else compute_mesh_size(dpg * n, degree))
-
     t_log0 = time.perf_counter()
 
     def log(msg):
@@ -105,178 +243,96 @@ def run(comm, a) -> dict | None:
             print(f"[bench {time.perf_counter() - t_log0:8.2f}s] {msg}", file=sys.stderr,
                   flush=True)
 
-    t_setup = time.perf_counter()
-    phase_t = {}
-
-    def mark(name):
-        phase_t[name] = time.perf_counter() - t_setup - sum(phase_t.values())
-
-    log(f"mesh {nx} degree {degree} fp{bits} on {n} rank(s)")
-    pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, a.perturb, a.kappa)
-    log(f"problem built (partition {pb.lat.pgrid}, {pb.partition})")
-    mark("problem")
-    u = pb.assemble_rhs()
-    x = pb.new_vector()
-    log("rhs assembled")
-    mark("rhs")
-    op = make_operator(pb, a.kernel, a.geometry)
-    log(f"operator {getattr(op, 'name', type(op).__name__)} ready")
-    mark("operator")
-
-    def sync():
-        if gpu:
-            torch.cuda.synchronize()
-        comm.barrier()
-        if gpu:
-            torch.cuda.synchronize()
-
-    if gpu:
-        cg = DeviceCG(pb)
-        cg.start(op, x, u)
-        cg.iterate(a.warmup)
-        cg.wait()
-    else:
-        cg_solve(op, pb, x, u, a.warmup, 0.0)
-    sync()
-    log("warmup done")
-    mark("warmup")
-    t_setup = time.perf_counter() - t_setup
-    t0 = time.perf_counter()
-    if gpu:
-        cg.iterate(a.steps)
-        cg.wait()  # bounded by the RCCL deadline: a hung peer raises
-    else:
-        cg_solve(op, pb, x, u, a.steps, 0.0)
-    sync()
-    dt = time.perf_counter() - t0
-    rank_dt = comm.gather_objects(dt)
-    dt = comm.allreduce_scalar(dt, "max")
-    value = pb.ndofs_global * a.steps / (1e9 * dt)
-    ynorm = pb.norm(x)
-    rt = getattr(op, "_rt", None)
-    runtime = (f"native C++ ({rt.transport}, hipGraph={rt.graphs}, overlap={rt.overlap}, "
-               f"tiled={rt.tiled})"
-               if rt is not None else "python")
-    comm_info = {"torch_backend": comm.backend, "torch_world": comm.size,
-                 "transport": rt.transport if rt is not None else "python",
-                 "rccl_ranks": rt.comm_ranks() if rt is not None else None,
-                 "halo_overlap": rt.overlap if rt is not None else False,
-                 "halo_bytes_per_exchange": pb.halo.bytes_per_exchange,
-                 "rank_ms_per_step_max": 1e3 * max(rank_dt) / a.steps,
-                 "rank_ms_per_step_min": 1e3 * min(rank_dt) / a.steps}
-    # phase attribution: a few extra eager iterations with hipEvent timers,
-    # after the timed loop and the norm (outside the measurement)
-    phases = phases_max = None
-    if rt is not None and a.profile_steps > 0:
-        phases = rt.profile(a.profile_steps)
-        allp = comm.gather_objects(phases)
-        phases_max = {k: (all(p[k] for p in allp) if isinstance(phases[k], bool)
-                          else max(p[k] for p in allp)) for k in phases}
-    if hasattr(op, "close"):
-        op.close()
-    px, py, pz = pb.lat.pgrid
-    mesh_nx, ndofs_global = list(nx), pb.ndofs_global
-    kname = getattr(op, "name", type(op).__name__)
-    geom = getattr(op, "geometry", "otf")
-    xseg = getattr(op, "nseg", None)
-    del op, x, u, pb, rt
-    if gpu:
-        del cg
-        torch.cuda.empty_cache()
+    head = _measure(comm, a, a.config, a.steps, a.warmup, kappa=a.kappa, perturb=a.perturb,
+                    kernel=a.kernel, geometry=a.geometry, profile_steps=a.profile_steps,
+                    log=log)
+    # the metric's second half: Q6 at 500 M DoFs/GPU, FP64 and FP32, on the
+    # same clock discipline as the headline (own steps / warmup / ms_per_step)
+    companions = {}
+    if a.companions == "on" or (a.companions == "auto" and a.config == "q3" and not a.mesh):
+        for c in ("q6", "q6f32"):
+            companions[c] = _guarded(comm, lambda c=c: _measure(
+                comm, a, c, a.steps, a.warmup, kappa=a.kappa, perturb=a.perturb,
+                kernel=a.kernel, geometry=a.geometry, log=log), log)
     extras = {}
-    if gpu and a.extras in ("on", "auto"):
-        # the north-star variants of the same config (BASELINE.json: random
-        # coefficients; the reference's --geom_perturb_fact general cells)
-        # "general" takes the auto kernel (fused3's x-trilinear instance on
-        # these meshes); "general_trilinear" forces the fully general
-        # trilinear-geometry instance on the same mesh
-        for key, kappa, pert, geo in (("random_kappa", "random", a.perturb, a.geometry),
-                                      ("general", a.kappa, a.perturb or 0.1, a.geometry),
-                                      ("general_trilinear", a.kappa, a.perturb or 0.1,
-                                       "otf-general")):
-            extras[key] = _variant(comm, a, nx, degree, dtype, kappa, pert, sync, log, geo)
+    if gpu and (a.extras == "on" or (a.extras == "auto" and n == 1)):
+        # north-star variants of the headline config (BASELINE.json: random
+        # coefficients; the reference's --geom_perturb_fact general cells; the
+        # reference's own data model).  "general" takes the auto kernel
+        # (fused3's x-trilinear instance on these meshes); "general_trilinear"
+        # forces the fully general trilinear-geometry instance on the same
+        # mesh; "dofmap" runs explicit cell->dof / cell->vertex arrays with G
+        # stored per quadrature point, as the reference does.
+        vsteps = min(a.steps, 50)
+        pert = a.perturb or 0.1
+        specs = (("random_kappa", a.config, dict(kappa="random", perturb=a.perturb)),
+                 ("general", a.config, dict(kappa=a.kappa, perturb=pert)),
+                 ("general_trilinear", a.config, dict(kappa=a.kappa, perturb=pert,
+                                                      geometry="otf-general")),
+                 ("dofmap", a.config, dict(kappa=a.kappa, perturb=a.perturb, kernel="dofmap",
+                                           geometry="stored")),
+                 ("q6_general", "q6", dict(kappa=a.kappa, perturb=pert)))
+        for key, cfg, kw in specs:
+            if cfg != a.config and (a.mesh or a.config != "q3"):
+                continue
+            kw.setdefault("kernel", a.kernel if kw.get("geometry") is None else "auto")
+            kw.setdefault("geometry", a.geometry)
+            extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure(
+                comm, a, cfg, vsteps, 3, log=log, **kw), log)
     if comm.rank != 0:
         return None
+    degree = head["degree"]
+    px, py, pz = head["partition"]
     return {
         "metric": "GDOF/s matrix-free Laplacian apply, Q3@300M & Q6@500M dofs/GPU, "
                   "1/2/4/8 MI355X",
-        "value": value,
+        "value": head["value"],
         "unit": "GDoF/s",
         "n_gpus": n,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": 1e3 * dt / a.steps,
+        "ms_per_step": head["ms_per_step"],
+        "ms_per_step_median": head["ms_per_step_median"],
+        "ms_per_step_min": head["ms_per_step_min"],
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": (value / (base * n)) if base else None,
-        "dtype": "fp64" if bits == 64 else "fp32",
+        "vs_baseline": head["vs_baseline"],
+        "dtype": head["dtype"],
         "data": "synthetic (box mesh + f = 1000 exp(-((x-.5)^2+(y-.5)^2)/.02), "
                 "as the reference)",
         "config": {
             "model": f"Q{degree} Poisson, qmode=1 GLL, matrix-free CG",
-            "global_batch": ndofs_global,
+            "global_batch": head["ndofs_global"],
             "seq_len": degree,
             "parallelism": f"dd{n} ({px}x{py}x{pz} box partition)",
-            "dofs_per_gpu": dpg,
-            "mesh": mesh_nx,
-            "kernel": kname,
-            "geometry": geom,
-            "x_segments": xseg,
-            "kappa": a.kappa,
-            "geom_perturb_fact": a.perturb,
-            "runtime": runtime,
-            "per_gpu_gdofs": value / n,
-            "y_norm": ynorm,
-            "setup_s": t_setup,
-            "setup_phases_s": phase_t,
+            "dofs_per_gpu": head["dofs_per_gpu"],
+            "mesh": head["mesh"],
+            "kernel": head["kernel"],
+            "geometry": head["geometry"],
+            "x_segments": head["x_segments"],
+            "kappa": head["kappa"],
+            "geom_perturb_fact": head["geom_perturb_fact"],
+            "runtime": head["runtime"],
+            "per_gpu_gdofs": head["value"] / n,
+            "y_norm": head["y_norm"],
+            "setup_s": head["setup_s"],
+            "setup_phases_s": head["setup_phases_s"],
             "device": _device_name() if gpu else "cpu",
             "build_flags": flags,
-            "comm": comm_info,
-            "phases_ms": phases,
-            "phases_ms_max_over_ranks": phases_max,
+            "comm": head["comm"],
+            "phases_ms": head.get("phases_ms"),
+            "phases_ms_max_over_ranks": head.get("phases_ms_max_over_ranks"),
         },
+        "q6_gdofs": companions.get("q6", {}).get("value"),
+        "q6f32_gdofs": companions.get("q6f32", {}).get("value"),
+        "companions": companions,
         "random_kappa_gdofs": extras.get("random_kappa", {}).get("value"),
         "general_gdofs": extras.get("general", {}).get("value"),
         "general_trilinear_gdofs": extras.get("general_trilinear", {}).get("value"),
+        "dofmap_gdofs": extras.get("dofmap", {}).get("value"),
+        "q6_general_gdofs": extras.get("q6_general", {}).get("value"),
         "variants": extras,
     }
-
-
-def _variant(comm, a, nx, degree, dtype, kappa, perturb, sync, log, geometry) -> dict:
-    """Time one variant of the headline config (same mesh and degree) with
-    its own operator and CG; min(steps, 50) timed iterations after 3 warmup."""
-    import torch
-
-    from benchmark_dolfinx_amd.driver import make_operator
-    from benchmark_dolfinx_amd.models.poisson import PoissonProblem
-    from benchmark_dolfinx_amd.solvers.cg import DeviceCG
-
-    pb = PoissonProblem(comm, nx, degree, 1, False, dtype, a.platform, perturb, kappa)
-    u = pb.assemble_rhs()
-    x = pb.new_vector()
-    op = make_operator(pb, a.kernel, geometry)
-    steps = min(a.steps, 50)
-    cg = DeviceCG(pb)
-    cg.start(op, x, u)
-    cg.iterate(3)
-    cg.wait()
-    sync()
-    t0 = time.perf_counter()
-    cg.iterate(steps)
-    cg.wait()
-    sync()
-    dt = comm.allreduce_scalar(time.perf_counter() - t0, "max")
-    rec = {"value": pb.ndofs_global * steps / (1e9 * dt), "ms_per_step": 1e3 * dt / steps,
-           "steps": steps, "kappa": kappa, "geom_perturb_fact": perturb,
-           "kernel": getattr(op, "name", type(op).__name__),
-           "geometry": getattr(op, "geometry", "otf"), "y_norm": pb.norm(x)}
-    log(f"variant kappa={kappa} perturb={perturb}: {rec['value']:.2f} GDoF/s "
-        f"({rec['kernel']}, {rec['geometry']})")
-    if hasattr(op, "close"):
-        op.close()
-    del op, cg, x, u, pb
-    torch.cuda.empty_cache()
-    return rec
 
 
 def _device_name() -> str:

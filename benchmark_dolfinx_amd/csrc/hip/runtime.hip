@@ -168,6 +168,9 @@ struct Transport {
   // communication), bounded by the transport's deadline.
   virtual int wait(hipEvent_t ev) { return static_cast<int>(hipEventSynchronize(ev)); }
   virtual bool aborted() const { return false; }
+  // Deadline watchdog whose Busy scopes must cover every host call that can
+  // block behind a stuck peer (RCCL only; null otherwise).
+  virtual bdx::Watchdog* watchdog() { return nullptr; }
 };
 
 double rccl_timeout_s() {
@@ -224,6 +227,7 @@ struct RcclTransport final : Transport {
     return 0;
   }
   bool aborted() const override { return was_aborted.load(); }
+  bdx::Watchdog* watchdog() override { return wd.get(); }
   int exchange(const void* sbuf, const std::vector<int64_t>& scnt,
                const std::vector<int64_t>& soff, void* rbuf, const std::vector<int64_t>& rcnt,
                const std::vector<int64_t>& roff, int esize, hipStream_t st) override {
@@ -296,6 +300,7 @@ struct ThreadGroupState {
   long generation = 0;
   std::vector<const void*> sbuf;
   std::vector<const std::vector<int64_t>*> soff;
+  std::vector<hipEvent_t> packed, copied;
   std::vector<double*> red;
   void barrier() {
     std::unique_lock<std::mutex> lk(m);
@@ -312,25 +317,52 @@ struct ThreadGroupState {
 std::mutex g_groups_m;
 std::map<int64_t, std::shared_ptr<ThreadGroupState>> g_groups;
 
+// The exchange is stream-ordered, as RCCL's: the host only swaps buffer
+// pointers and event handles at two barriers and never waits for the device,
+// so the compute stream's interior tiles really run while the copies do.
+//   1. record `packed` on the caller's stream (after the pack kernel);
+//   2. barrier: every rank's send buffer / offsets / `packed` are published;
+//   3. per peer: wait for its `packed`, copy its slice into the receive buffer;
+//      record `copied`;
+//   4. barrier: every `copied` is published; wait for the `copied` of each
+//      peer that reads this rank's send buffer, so a later write to it (the
+//      next pack, stream-ordered after this) cannot overtake their copies.
+// Event reuse is safe: a rank re-records `packed` only after barrier 2 of
+// the previous exchange (every peer's wait on it was issued before that
+// barrier) and `copied` only after barrier 1 of the next exchange (every
+// peer issues its wait on it before arriving there).
 struct ThreadTransport final : Transport {
   std::shared_ptr<ThreadGroupState> g;
   int rank = 0;
+  hipEvent_t ev_packed = nullptr, ev_copied = nullptr;
+  ~ThreadTransport() override {
+    if (ev_packed) hipEventDestroy(ev_packed);
+    if (ev_copied) hipEventDestroy(ev_copied);
+  }
   int exchange(const void* sbuf, const std::vector<int64_t>& scnt,
                const std::vector<int64_t>& soff, void* rbuf, const std::vector<int64_t>& rcnt,
                const std::vector<int64_t>& roff, int esize, hipStream_t st) override {
-    (void)scnt;
-    BDX_CHECK(hipStreamSynchronize(st));
+    if (!ev_packed) {
+      BDX_CHECK(hipEventCreateWithFlags(&ev_packed, hipEventDisableTiming));
+      BDX_CHECK(hipEventCreateWithFlags(&ev_copied, hipEventDisableTiming));
+    }
+    BDX_CHECK(hipEventRecord(ev_packed, st));
     g->sbuf[rank] = sbuf;
     g->soff[rank] = &soff;
+    g->packed[rank] = ev_packed;
     g->barrier();
     for (int p = 0; p < g->size; ++p) {
       if (rcnt[p] <= 0) continue;
       const char* src = static_cast<const char*>(g->sbuf[p]) + (*g->soff[p])[rank] * esize;
+      BDX_CHECK(hipStreamWaitEvent(st, g->packed[p], 0));
       BDX_CHECK(hipMemcpyAsync(static_cast<char*>(rbuf) + roff[p] * esize, src, rcnt[p] * esize,
                                hipMemcpyDeviceToDevice, st));
     }
-    BDX_CHECK(hipStreamSynchronize(st));
+    BDX_CHECK(hipEventRecord(ev_copied, st));
+    g->copied[rank] = ev_copied;
     g->barrier();
+    for (int p = 0; p < g->size; ++p)
+      if (scnt[p] > 0) BDX_CHECK(hipStreamWaitEvent(st, g->copied[p], 0));
     return 0;
   }
   int allreduce_sum(double* dev, int n, hipStream_t st) override {
@@ -424,6 +456,8 @@ struct CGRuntime {
   bool x_lag = false;
   bool use_graph = true, graph_ok[2] = {false, false};
   hipGraphExec_t graph[2] = {nullptr, nullptr};
+  hipEvent_t ev_batch[2] = {nullptr, nullptr};  // in-flight bound (iterate_on_stream)
+  std::vector<hipEvent_t> tev;                  // per-step timing events
 
   void mark(int id, hipStream_t s) {
     if (prof) (void)hipEventRecord(pev[id], s);
@@ -582,35 +616,66 @@ struct CGRuntime {
     }
   }
 
-  int iterate(long n) {
+  // n iterations; step_ms (may be null): n per-step device times from
+  // timing events recorded between the iterations (no extra work, no sync)
+  int iterate(long n, float* step_ms = nullptr) {
     if (tr->aborted()) return kErrAborted;
     BDX_CHECK(hipEventRecord(ev_in, ext));
     BDX_CHECK(hipStreamWaitEvent(st, ev_in, 0));
-    int rc = iterate_on_stream(n);
+    int rc = iterate_on_stream(n, step_ms);
     BDX_CHECK(hipEventRecord(ev_out, st));
     BDX_CHECK(hipStreamWaitEvent(ext, ev_out, 0));
+    if (!rc && step_ms) {
+      if ((rc = tr->wait(ev_out))) return rc;
+      for (long i = 0; i < n; ++i) {
+        BDX_CHECK(hipEventElapsedTime(&step_ms[i], tev[i], tev[i + 1]));
+      }
+    }
     return rc;
   }
 
-  int iterate_on_stream(long n) {
+  // Iterations are enqueued in batches of kBatch under a watchdog Busy
+  // scope, and before each batch the host waits (bounded by the deadline)
+  // for the batch before the previous one: at most 2 kBatch iterations are
+  // in flight, so an enqueue can never block for long behind a stuck peer
+  // outside a deadline-covered scope, and a long run never trips it.
+  static constexpr long kBatch = 32;
+  int iterate_on_stream(long n, float* step_ms) {
     if (int rc = import_state()) return rc;
-    for (long i = 0; i < n; ++i) {
-      const bool first = (it == 0);
-      const int par = static_cast<int>(it % 2);
-      const bool steady = !first && x_lag && !prof;
-      if (steady && use_graph && tr->capturable() && !graph_ok[par]) {
-        graph_ok[par] = capture(par);
-        if (!graph_ok[par]) use_graph = false;  // fall back to eager launches
+    if (step_ms) {
+      while (static_cast<long>(tev.size()) < n + 1) {
+        hipEvent_t e = nullptr;
+        BDX_CHECK(hipEventCreate(&e));
+        tev.push_back(e);
       }
-      if (steady && use_graph && graph_ok[par]) {
-        BDX_CHECK(hipGraphLaunch(graph[par], st));
-      } else {
-        const int rc = step(it, first, x_lag);
-        if (rc) return rc;
-      }
-      x_lag = true;
-      ++it;
+      BDX_CHECK(hipEventRecord(tev[0], st));
     }
+    for (long i0 = 0; i0 < n; i0 += kBatch) {
+      if (i0 >= 2 * kBatch) {
+        if (int rc = tr->wait(ev_batch[(i0 / kBatch) % 2])) return rc;
+      }
+      bdx::Watchdog::Busy busy(tr->watchdog());
+      for (long i = i0; i < n && i < i0 + kBatch; ++i) {
+        const bool first = (it == 0);
+        const int par = static_cast<int>(it % 2);
+        const bool steady = !first && x_lag && !prof;
+        if (steady && use_graph && tr->capturable() && !graph_ok[par]) {
+          graph_ok[par] = capture(par);
+          if (!graph_ok[par]) use_graph = false;  // fall back to eager launches
+        }
+        if (steady && use_graph && graph_ok[par]) {
+          BDX_CHECK(hipGraphLaunch(graph[par], st));
+        } else {
+          const int rc = step(it, first, x_lag);
+          if (rc) return rc;
+        }
+        x_lag = true;
+        ++it;
+        if (step_ms) BDX_CHECK(hipEventRecord(tev[i + 1], st));
+      }
+      BDX_CHECK(hipEventRecord(ev_batch[(i0 / kBatch) % 2], st));
+    }
+    bdx::Watchdog::Busy busy(tr->watchdog());
     return flush();
   }
 
@@ -642,7 +707,14 @@ struct CGRuntime {
     for (int i = 0; i < nout; ++i) out[i] = 0.0;
     BDX_CHECK(hipEventRecord(ev_in, ext));
     BDX_CHECK(hipStreamWaitEvent(st, ev_in, 0));
+    // prof is cleared on every exit path (an early error return must not
+    // leave later iterate() calls eager and recording phase events)
+    struct ProfGuard {
+      bool& f;
+      ~ProfGuard() { f = false; }
+    } guard{prof};
     prof = true;
+    bdx::Watchdog::Busy busy(tr->watchdog());
     int rc = import_state();
     for (long i = 0; i < n && !rc; ++i) {
       const bool first = (it == 0);
@@ -650,7 +722,7 @@ struct CGRuntime {
       if (rc) break;
       x_lag = true;
       ++it;
-      BDX_CHECK(hipEventRecord(ev_out, st));
+      if ((rc = static_cast<int>(hipEventRecord(ev_out, st)))) break;
       if ((rc = tr->wait(ev_out))) break;
       auto dt = [&](int a, int b) {
         float ms = 0.f;
@@ -686,7 +758,8 @@ struct CGRuntime {
     drop_graphs();
     for (auto& e : pev)
       if (e) hipEventDestroy(e);
-    for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_fwd, ev_bnd, ev_rev})
+    for (hipEvent_t e : tev) hipEventDestroy(e);
+    for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_fwd, ev_bnd, ev_rev, ev_batch[0], ev_batch[1]})
       if (e) hipEventDestroy(e);
     if (st) hipStreamDestroy(st);
     if (cs) hipStreamDestroy(cs);
@@ -782,7 +855,7 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
       hipStreamCreateWithFlags(&rt->cs, hipStreamNonBlocking) != hipSuccess)
     return nullptr;
   for (hipEvent_t* e : {&rt->ev_in, &rt->ev_out, &rt->ev_fork, &rt->ev_fwd, &rt->ev_bnd,
-                        &rt->ev_rev})
+                        &rt->ev_rev, &rt->ev_batch[0], &rt->ev_batch[1]})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
   rt->face_cnt.assign(face_cnt, face_cnt + nranks);
   rt->ghost_cnt.assign(ghost_cnt, ghost_cnt + nranks);
@@ -822,6 +895,8 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
         g->size = nranks;
         g->sbuf.assign(nranks, nullptr);
         g->soff.assign(nranks, nullptr);
+        g->packed.assign(nranks, nullptr);
+        g->copied.assign(nranks, nullptr);
         g->red.assign(nranks, nullptr);
       }
       t->g = g;
@@ -968,6 +1043,12 @@ int bdx_rt_bind_x(void* h, void* x) {
 
 int bdx_rt_iterate(void* h, long n) {
   return with_rt(h, [&](auto* rt) { return rt->iterate(n); });
+}
+
+// iterate() plus the device time of each of the n steps (timing events
+// between the steps, read after a bounded host wait): step_ms[n]
+int bdx_rt_iterate_timed(void* h, long n, float* step_ms) {
+  return with_rt(h, [&](auto* rt) { return rt->iterate(n, step_ms); });
 }
 
 // Host wait for everything iterate() queued, bounded by the RCCL deadline

@@ -83,6 +83,7 @@ def declare(lib) -> None:
     _d(lib, "bdx_rt_profile", [vp, ctypes.c_long, vp, i32])
     _d(lib, "bdx_rt_reset", [vp])
     _d(lib, "bdx_rt_iterate", [vp, ctypes.c_long])
+    _d(lib, "bdx_rt_iterate_timed", [vp, ctypes.c_long, vp])
     _d(lib, "bdx_rt_state", [vp, vp, vp])
     _d(lib, "bdx_rt_destroy", [vp], None)
     _d(lib, "bdx_rt_release_group", [i64], None)

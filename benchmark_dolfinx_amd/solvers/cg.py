@@ -99,6 +99,24 @@ class DeviceCG:
             k.p_update(p, r, scal, nxt, cur)
             self.it += 1
 
+    def iterate_timed(self, n: int) -> list[float]:
+        """iterate(n) plus the device time (ms) of each step.  The native
+        runtime records timing events between its steps (same launches as
+        iterate); the Python loop records torch events around each step."""
+        rt = getattr(self.op, "_rt", None)
+        if rt is not None:
+            return rt.iterate_timed(n)
+        if self.pb.platform != "gpu":
+            self.iterate(n)
+            return []
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        ev[0].record()
+        for i in range(n):
+            self.iterate(1)
+            ev[i + 1].record()
+        ev[n].synchronize()
+        return [ev[i].elapsed_time(ev[i + 1]) for i in range(n)]
+
     def wait(self) -> None:
         """Host wait for the queued iterations.  With the native runtime the
         wait is bounded by the RCCL deadline (a hung peer raises instead of

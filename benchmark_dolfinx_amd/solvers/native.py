@@ -183,6 +183,14 @@ class NativeCGRuntime:
         _check(self.lib.bdx_rt_iterate(self.h, int(n)), "rt_iterate")
         self._sync_state()
 
+    def iterate_timed(self, n: int) -> list[float]:
+        """iterate(n) and return the device time (ms) of each step, from
+        timing events recorded between the steps (waits for the steps)."""
+        out = (ctypes.c_float * max(1, int(n)))()
+        _check(self.lib.bdx_rt_iterate_timed(self.h, int(n), out), "rt_iterate_timed")
+        self._sync_state()
+        return [float(v) for v in out[:int(n)]]
+
     def wait(self) -> None:
         """Host wait for the queued iterations, bounded by the RCCL deadline
         (BDX_RCCL_TIMEOUT_S): a hung peer raises instead of blocking forever."""
@@ -200,7 +208,11 @@ class NativeCGRuntime:
 
     def close(self) -> None:
         if getattr(self, "h", None):
-            torch.cuda.synchronize()
+            # bounded by the RCCL deadline (a hung peer must not block the
+            # teardown forever), then the device for the caller's stream
+            rc = self.lib.bdx_rt_wait(self.h)
+            if rc == 0:
+                torch.cuda.synchronize()
             self.lib.bdx_rt_destroy(self.h)
             self.h = None
         if getattr(self, "group", 0):

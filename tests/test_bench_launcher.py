@@ -39,6 +39,18 @@ def test_self_launch_four_ranks_matches_one_rank():
     common = ["--steps", "3", "--warmup", "1", "--profile-steps", "0"]
     one = _line(_bench(["--gpus", "1", "--dofs-per-gpu", "24000", *common]))
     four = _line(_bench(["--gpus", "4", "--dofs-per-gpu", "6000", *common]))
+    # the metric's Q6 half rides along (own steps / ms_per_step), FP64 and
+    # FP32, partition-invariant like the headline
+    for rec in (one, four):
+        for c in ("q6", "q6f32"):
+            comp = rec["companions"][c]
+            assert comp.get("error") is None, comp
+            assert comp["steps"] == 3 and comp["warmup"] == 1 and comp["degree"] == 6
+            assert comp["dtype"] == ("fp64" if c == "q6" else "fp32")
+            assert rec[f"{c}_gdofs"] == comp["value"] > 0
+    for c, tol in (("q6", 1e-12), ("q6f32", 1e-4)):
+        a, b = one["companions"][c]["y_norm"], four["companions"][c]["y_norm"]
+        assert abs(a - b) <= tol * abs(a), (c, a, b)
     assert one["n_gpus"] == 1 and four["n_gpus"] == 4
     assert four["config"]["comm"]["torch_world"] == 4
     assert four["config"]["comm"]["torch_backend"] == "gloo"
@@ -49,6 +61,23 @@ def test_self_launch_four_ranks_matches_one_rank():
     assert abs(y1 - y4) <= 1e-12 * abs(y1), (y1, y4)
     c = four["config"]["comm"]
     assert c["rank_ms_per_step_max"] >= c["rank_ms_per_step_min"] > 0
+
+
+def test_self_launch_eight_ranks_yz_partition():
+    """The 8-GPU driver run's shape on the CPU: 8 self-launched ranks, x kept
+    whole (1 x 2 x 4, the GPU partition policy), same CG iterate as 1 rank."""
+    common = ["--steps", "2", "--warmup", "1", "--profile-steps", "0", "--companions", "off"]
+    one = _line(_bench(["--gpus", "1", "--dofs-per-gpu", "24000", *common]))
+    eight = _line(_bench(["--gpus", "8", "--dofs-per-gpu", "3000", *common], timeout=400,
+                         BDX_PARTITION="yz"))
+    assert eight["n_gpus"] == 8
+    # x whole, y and z both split (1x2x4 on the GPU's meshes; 1x4x2 here)
+    assert eight["config"]["parallelism"].split()[1] in ("(1x2x4", "(1x4x2")
+    assert eight["config"]["comm"]["torch_world"] == 8
+    assert eight["config"]["mesh"] == one["config"]["mesh"]
+    y1, y8 = one["config"]["y_norm"], eight["config"]["y_norm"]
+    assert abs(y1 - y8) <= 1e-12 * abs(y1), (y1, y8)
+    assert eight["q6_gdofs"] is None and not eight["companions"]
 
 
 def test_self_launch_kills_siblings_when_a_rank_fails():
