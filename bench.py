@@ -232,10 +232,10 @@ def run(comm, a) -> dict | None:
     if gpu:
         from benchmark_dolfinx_amd.ops.native import build_flags
         flags = build_flags()
-        if not flags["valid"] and os.environ.get("BDX_ALLOW_DROP") != "1":
-            raise SystemExit(f"bench.py: the HIP library was built with timing-only phase "
-                             f"drops {flags['drops']} (wrong numerics); refusing to time it "
-                             f"(BDX_ALLOW_DROP=1 runs it, marked invalid)")
+        if not flags["valid"] and os.environ.get("BDX_ALLOW_VARIANT") != "1":
+            raise SystemExit(f"bench.py: the loaded HIP library is not the production build "
+                             f"({flags}); refusing to time it (BDX_ALLOW_VARIANT=1 runs it, "
+                             f"marked invalid)")
     t_log0 = time.perf_counter()
 
     def log(msg):

@@ -48,30 +48,18 @@ enum { kGeomStored = 0, kGeomOTF = 1 };
 #endif
 
 // Streamed vectors (read or written once per CG iteration; every vector is
-// far larger than the 256 MiB Infinity Cache): BDX_NT bit 1 = non-temporal
-// loads, bit 2 = non-temporal stores.  Default 0: non-temporal loads AND
-// stores measured 36-37 % SLOWER on all three headline configs (Q3 46.7 ->
+// far larger than the 256 MiB Infinity Cache) use the default cache policy:
+// non-temporal loads AND stores measured 36-37 % SLOWER on all three headline configs (Q3 46.7 ->
 // 29.9, Q6 44.6 -> 28.9, Q6-FP32 59.3 -> 35.1 GDoF/s, profiles/r2_nt_ab.md):
 // the x-march writes 96-byte row segments, and only the default policy lets
 // L2 merge neighbouring tiles' segments into whole lines before write-back.
-#ifndef BDX_NT
-#define BDX_NT 0
-#endif
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-#if BDX_NT & 1
-  return __builtin_nontemporal_load(p);
-#else
   return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void st_stream(T* p, T v) {
-#if BDX_NT & 2
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 // 1D operator tables, passed by value as a kernel argument (< 1.5 KiB).

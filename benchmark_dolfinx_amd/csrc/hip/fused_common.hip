@@ -23,99 +23,21 @@ int pack_tables(const double* phi0, const double* dphi1, T* out) {
 }
 
 
-// Timing-only drops for A/B attribution (wrong numerics when nonzero):
-// 1 = tile-interface fold, 2 = r.r (scripts/job_upddrop.sh)
-#ifndef BDX_UPD_DROP
-#define BDX_UPD_DROP 0
-#endif
-
-// Flat non-persistent update pass (1) or the row kernel (0); kPartialsCap is
-// the partials capacity every caller provides (bdx_hip_partials_size).  The
-// flat pass wants a non-persistent grid (a persistent 8192/16384-block
+// kPartialsCap is the partials capacity every caller provides
+// (bdx_hip_partials_size).  The flat update pass wants a non-persistent grid (a persistent 8192/16384-block
 // grid-stride version measured 1.70 ms vs 1.52 at Q3); its up to 65280 block
 // partials are summed in two fixed-order stages (256 slices into the last 256
 // slots of the partials buffer, then one block): deterministic like the rest.
-#ifndef BDX_UPD_FLAT
-#define BDX_UPD_FLAT 1
-#endif
 constexpr int kPartialsCap = 65536, kStage1 = 256;
-#ifndef BDX_UPD_GRID
-#define BDX_UPD_GRID (kPartialsCap - kStage1)
-#endif
-static_assert(BDX_UPD_GRID <= kPartialsCap - kStage1, "update grid exceeds the partials capacity");
+constexpr int kUpdGrid = kPartialsCap - kStage1;  // update pass grid cap
 
-// CG update of the fused2 path: alpha = s[rn] / s[pap];
+// CG update of the fused2..5 paths: alpha = s[rn] / s[pap];
 //   r -= alpha (y + interface partials);  partial r.r
 // The tile-interface partials (YB/ZB/CB) are folded here on the fly instead of
 // by a separate finalize pass over y (same sum as fused_finalize_kernel).
-// x is not touched: its update x += alpha p is lagged into the next fused2
+// x is not touched: its update x += alpha p is lagged into the next fused
 // launch (staging reads p there anyway) and flushed by bdx_xflush at the end.
-template <typename T>
-__global__ void __launch_bounds__(256)
-    cg_update_iface_kernel(int64_t L1, int64_t ld, int64_t o0, int64_t o1, int64_t o2,
-                           int64_t Lz, T* __restrict__ r, const T* __restrict__ y,
-                           const T* __restrict__ yb, const T* __restrict__ zb,
-                           const T* __restrict__ cb, int nty, int ntz, int sy, int sz,
-                           const double* __restrict__ scal, int rn_slot, int pap_slot,
-                           double* __restrict__ partials) {
-  __shared__ double lds[16];
-  const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t nrows = o0 * o1;
-  const float inv_sz = 1.0f / static_cast<float>(sz);
-  double acc = 0.0;
-  for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + wid; row < nrows;
-       row += static_cast<int64_t>(gridDim.x) * 4) {
-    const int64_t i = row / o1, j = row - i * o1;
-    const int64_t base = (i * L1 + j) * ld;
-    const int tyy = static_cast<int>(j / sy);
-    const int yrow = (j % sy == 0 && tyy >= 1 && tyy < nty) ? tyy - 1 : -1;
-    const T* __restrict__ ybr = yb + (i * (nty - 1) + (yrow < 0 ? 0 : yrow)) * Lz;
-    const T* __restrict__ zbr = zb + (i * L1 + j) * (ntz - 1);
-    const T* __restrict__ cbr = cb + (i * (nty - 1) + (yrow < 0 ? 0 : yrow)) * (ntz - 1);
-    // 16-byte vectors along the row (rows start 128-byte aligned: the storage
-    // pitch ld is a multiple of 16 elements); per element the interface terms
-    constexpr int W = 16 / sizeof(T);
-    typedef T V __attribute__((ext_vector_type(W)));
-    for (int k0 = lane * W; k0 < o2; k0 += 64 * W) {
-      const bool full = k0 + W <= o2;
-      V vy, vr;
-      if (full) {
-        vy = *reinterpret_cast<const V*>(y + base + k0);
-        vr = *reinterpret_cast<const V*>(r + base + k0);
-      }
-#pragma unroll
-      for (int e = 0; e < W; ++e) {
-        const int k = k0 + e;
-        if (k >= o2) break;
-        T v = full ? vy[e] : y[base + k];
-#if (BDX_UPD_DROP & 1) == 0
-        if (yrow >= 0) v += ybr[k];
-        int zq = static_cast<int>(static_cast<float>(k) * inv_sz);
-        if (zq * sz > k) --zq;
-        if ((zq + 1) * sz <= k) ++zq;
-        if (zq * sz == k && zq >= 1 && zq < ntz) {
-          v += zbr[zq - 1];
-          if (yrow >= 0) v += cbr[zq - 1];
-        }
-#endif
-        const T rn = (full ? vr[e] : r[base + k]) - alpha * v;
-        if (full)
-          vr[e] = rn;
-        else
-          r[base + k] = rn;
-#if (BDX_UPD_DROP & 2) == 0
-        acc += static_cast<double>(rn) * static_cast<double>(rn);
-#endif
-      }
-      if (full) *reinterpret_cast<V*>(r + base + k0) = vr;
-    }
-  }
-  const double t = block_sum(acc, lds);
-  if (threadIdx.x == 0) partials[blockIdx.x] = t;
-}
-
-// Flat variant of the update (BDX_UPD_FLAT): the owned rows j < o1 of an
+// Flat pass (a row-per-wave kernel measured slower): the owned rows j < o1 of an
 // x-plane are one contiguous block of o1 * ld elements (row pitch ld, a
 // multiple of 16 elements: no 16-byte vector straddles two rows), so the pass
 // runs as a plain stream -- one chunk of 256 threads x 2 vectors per block,
@@ -326,20 +248,14 @@ extern "C" {
                                 double* partials, hipStream_t st) {                 \
     const BdxLattice lat = BdxLattice::from(latd);                                  \
     int g;                                                                          \
-    if (BDX_UPD_FLAT) {                                                             \
+    {                                                             \
       const int64_t nvp = own[1] * (lat.ld * static_cast<int64_t>(sizeof(T)) / 16); \
       const int64_t want = own[0] * ((nvp + 511) / 512);                            \
-      g = static_cast<int>(want < BDX_UPD_GRID ? (want > 0 ? want : 1) : BDX_UPD_GRID); \
+      g = static_cast<int>(want < kUpdGrid ? (want > 0 ? want : 1) : kUpdGrid); \
       cg_update_flat_kernel<T><<<g, 256, 0, st>>>(lat.L[1], lat.ld, own[0], own[1], \
                                                   own[2], lat.L[2], r, y, yb, zb, cb, \
                                                   nty, ntz, sy, sz, scal, rn_slot,  \
                                                   pap_slot, partials);              \
-    } else {                                                                        \
-      g = rows_grid(own[0] * own[1]);                                               \
-      cg_update_iface_kernel<T><<<g, 256, 0, st>>>(lat.L[1], lat.ld, own[0], own[1], \
-                                                   own[2], lat.L[2], r, y, yb, zb, cb, \
-                                                   nty, ntz, sy, sz, scal, rn_slot, \
-                                                   pap_slot, partials);             \
     }                                                                               \
     if (g > 4 * kStage1) {                                                          \
       double* stage = partials + kPartialsCap - kStage1;                            \
@@ -373,7 +289,7 @@ BDX_CGI(float, f32)
       return static_cast<int>(hipErrorInvalidValue);                                           \
     const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
     const int64_t want = (nvec + 255) / 256;                                                   \
-    const int g = static_cast<int>(want < BDX_UPD_GRID ? (want > 0 ? want : 1) : BDX_UPD_GRID); \
+    const int g = static_cast<int>(want < kUpdGrid ? (want > 0 ? want : 1) : kUpdGrid); \
     cg_update_tiled_kernel<T><<<g, 256, 0, st>>>(                                              \
         L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),              \
         static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,    \
@@ -401,16 +317,6 @@ BDX_CGT(float, f32)
 #undef BDX_CGT
 
 // Timing-only phase drops compiled into this TU (0 in a valid build).
-int bdx_drop_flags_common() { return BDX_UPD_DROP; }
-// Timing-only stage drops of the fused2 / fused3 cores (BDX_X_*, BDX_X3_*),
-// one bit each; nonzero = wrong numerics (bench.py refuses to time it).
-int bdx_drop_flags_f23() {
-  return (BDX_X_NOSTAGE ? 1 : 0) | (BDX_X_NOOUT ? 2 : 0) | (BDX_X_NOFRONT ? 4 : 0) |
-         (BDX_X_NOGRAD ? 8 : 0) | (BDX_X_NOTGRAD ? 16 : 0) | (BDX_X_NOBACK ? 32 : 0) |
-         (BDX_X3_NOFZ ? 64 : 0) | (BDX_X3_NOFY ? 128 : 0) | (BDX_X3_NOXF ? 256 : 0) |
-         (BDX_X3_NOBY ? 512 : 0) | (BDX_X3_NOBZ ? 1024 : 0) | (BDX_X3_NOSYNC ? 2048 : 0);
-}
-
 // Tile shape (cells in y, z) used by the fused kernel for a given nq.
 int bdx_fused_tile(int nq, int* ty, int* tz) {
   switch (nq) {

@@ -31,15 +31,6 @@
 
 enum { kFusedAction = 0, kFusedCG = 1 };
 
-#ifndef BDX_FAST_RCP
-#define BDX_FAST_RCP 0
-#endif
-#ifndef BDX_TAB_LDS
-#define BDX_TAB_LDS 0
-#endif
-#ifndef BDX_EXP_NOGEOM
-#define BDX_EXP_NOGEOM 0
-#endif
 
 // 1/x from the hardware reciprocal estimate + two Newton steps (full
 // precision for the normal, positive Jacobian determinants seen here) instead
@@ -76,26 +67,17 @@ __device__ __forceinline__ float fast_rcp(float x) {
     __builtin_amdgcn_sched_barrier(0);                 \
   } while (0)
 
-#ifndef BDX_NO_SCHED_FENCE
 #define BDX_SCHED_FENCE()               \
   do {                                  \
     asm volatile("" ::: "memory");      \
     __builtin_amdgcn_sched_barrier(0);  \
   } while (0)
-#else
-#define BDX_SCHED_FENCE()
-#endif
 
 // Minimum waves per SIMD requested from the register allocator (the LDS
-// footprint allows 3 workgroups/CU up to nq=6 and 2 beyond).  Override with
-// -DBDX_FUSED_WAVES=n for experiments.
+// footprint allows 3 workgroups/CU up to nq=6 and 2 beyond).
 template <int NQ>
 struct FusedWaves {
-#ifdef BDX_FUSED_WAVES
-  static constexpr int value = BDX_FUSED_WAVES;
-#else
   static constexpr int value = NQ <= 6 ? 3 : 2;
-#endif
 };
 
 template <typename T> struct VecOf;
@@ -161,11 +143,7 @@ template <int NQ> struct TileFor;
 template <> struct TileFor<2> { static constexpr int TY = 8, TZ = 8; };
 template <> struct TileFor<3> { static constexpr int TY = 4, TZ = 7; };
 template <> struct TileFor<4> { static constexpr int TY = 4, TZ = 4; };
-#ifndef BDX_TILE5_TY
-#define BDX_TILE5_TY 2
-#define BDX_TILE5_TZ 5
-#endif
-template <> struct TileFor<5> { static constexpr int TY = BDX_TILE5_TY, TZ = BDX_TILE5_TZ; };
+template <> struct TileFor<5> { static constexpr int TY = 2, TZ = 5; };
 template <> struct TileFor<6> { static constexpr int TY = 1, TZ = 7; };
 template <> struct TileFor<7> { static constexpr int TY = 1, TZ = 5; };
 template <> struct TileFor<8> { static constexpr int TY = 2, TZ = 2; };
@@ -359,11 +337,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
     // inside the layer instead of pinning them for the whole x-march.
     int toff = 0;
     asm volatile("" : "+s"(toff));
-#if BDX_TAB_LDS
-    const T* __restrict__ gt = s_tab + toff;   // uniform rows as LDS broadcast reads
-#else
     const T* __restrict__ gt = tb.tab + toff;  // wave-uniform rows -> SMEM (kernarg)
-#endif
     const T* __restrict__ su = s_u[cur];
     const T* __restrict__ sX = s_X[cur];
 
@@ -491,11 +465,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         const T K10 = J12 * J20 - J10 * J22, K11 = J00 * J22 - J02 * J20, K12 = J02 * J10 - J00 * J12;
         const T K20 = J10 * J21 - J11 * J20, K21 = J01 * J20 - J00 * J21, K22 = J00 * J11 - J01 * J10;
         const T det = J00 * K00 + J01 * K10 + J02 * K20;
-#if BDX_FAST_RCP
-        const T sc = kwyz * s_qw[NQ + q] * fast_rcp(det);
-#else
         const T sc = kwyz * s_qw[NQ + q] / det;
-#endif
         // h = K^T g, F = sc K h  (= kappa w det J^-1 J^-T g)
         const T h0 = K00 * gx[q] + K10 * gy[q] + K20 * gz[q];
         const T h1 = K01 * gx[q] + K11 * gy[q] + K21 * gz[q];
@@ -503,11 +473,6 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         fx = sc * (K00 * h0 + K01 * h1 + K02 * h2);
         fy = sc * (K10 * h0 + K11 * h1 + K12 * h2);
         fz = sc * (K20 * h0 + K21 * h1 + K22 * h2);
-#if BDX_EXP_NOGEOM  // timing experiment only: wrong numerics
-        fx = kwyz * gx[q];
-        fy = kwyz * gy[q];
-        fz = kwyz * gz[q];
-#endif
       } else {
         T Gd[6] = {0, 0, 0, 0, 0, 0};
         if (cell_on) {

@@ -20,32 +20,10 @@
 #pragma once
 #include "lap_fused.h"
 
-// Unroll factor of the LDS-fed contraction loops (rolled by default: keeps the
-// register budget of 3 waves/SIMD).  Timing-experiment switches BDX_X_* drop
-// a phase (WRONG numerics; only for attributing time on the GPU box).
-#ifndef BDX_MUNROLL
-#define BDX_MUNROLL 1
-#endif
+// The LDS-fed contraction loops stay rolled (BDX_PRAGMA_UNROLL(1)): keeps the
+// register budget of 3 waves/SIMD.
 #define BDX_PRAGMA(x) _Pragma(#x)
 #define BDX_PRAGMA_UNROLL(n) BDX_PRAGMA(unroll n)
-#ifndef BDX_X_NOSTAGE
-#define BDX_X_NOSTAGE 0
-#endif
-#ifndef BDX_X_NOOUT
-#define BDX_X_NOOUT 0
-#endif
-#ifndef BDX_X_NOFRONT
-#define BDX_X_NOFRONT 0
-#endif
-#ifndef BDX_X_NOGRAD
-#define BDX_X_NOGRAD 0
-#endif
-#ifndef BDX_X_NOTGRAD
-#define BDX_X_NOTGRAD 0
-#endif
-#ifndef BDX_X_NOBACK
-#define BDX_X_NOBACK 0
-#endif
 
 template <typename T>
 struct Fused2Args {
@@ -347,7 +325,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
-      if (!BDX_X_NOSTAGE && !last && (st_meta[k] & kValid)) {
+      if (!last && (st_meta[k] & kValid)) {
         pf_r[k] = A.u[lnext + st_goff[k]];
         if constexpr (MODE == kFusedCG) {
           pf_p[k] = A.pold[lnext + st_goff[k]];
@@ -379,10 +357,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
 
     // ------------------------------------------------ interpolate to qpts
     T U[NQ];
-    if constexpr (BDX_X_NOFRONT) {
-#pragma unroll
-      for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[(i % ND) * PLP + (b % ND)] : T(0);
-    } else if constexpr (IDENT) {
+    if constexpr (IDENT) {
 #pragma unroll
       for (int i = 0; i < NQ; ++i) U[i] = lane_on ? ua[i * PLP + b] : T(0);
     } else {
@@ -391,7 +366,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
         T o[ND];
 #pragma unroll
         for (int i = 0; i < ND; ++i) o[i] = 0;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
+BDX_PRAGMA_UNROLL(1)
         for (int k = 0; k < ND; ++k) {
           const T cc = ph[k];
 #pragma unroll
@@ -404,7 +379,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
       T t2[ND];
 #pragma unroll
       for (int i = 0; i < ND; ++i) t2[i] = 0;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
+BDX_PRAGMA_UNROLL(1)
       for (int j = 0; j < ND; ++j) {
         T row[ND];
         ldrow<ND>(w1b + j * NQ * XP, row);
@@ -429,9 +404,9 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
       const T* __restrict__ dra = s_tab + S::OFF_DR + a * XP;
       const T* __restrict__ drb = s_tab + S::OFF_DR + b * XP;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) gx[q] = gy[q] = gz[q] = BDX_X_NOGRAD ? U[q] : T(0);
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-      for (int m = 0; m < (BDX_X_NOGRAD ? 0 : NQ); ++m) {
+      for (int q = 0; q < NQ; ++q) gx[q] = gy[q] = gz[q] = T(0);
+BDX_PRAGMA_UNROLL(1)
+      for (int m = 0; m < NQ; ++m) {
         T ry[NQ], rz[NQ];
         ldrow<NQ>(w2b + m * NQ * XP, ry);
         ldrow<NQ>(w2a + m * XP, rz);
@@ -593,9 +568,9 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
       const T* __restrict__ dca = s_tab + S::OFF_DC + a * XP;
       const T* __restrict__ dcb = s_tab + S::OFF_DC + b * XP;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) r[q] = BDX_X_NOTGRAD ? Fx[q] : T(0);
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
-      for (int m = 0; m < (BDX_X_NOTGRAD ? 0 : NQ); ++m) {
+      for (int q = 0; q < NQ; ++q) r[q] = T(0);
+BDX_PRAGMA_UNROLL(1)
+      for (int m = 0; m < NQ; ++m) {
         T r1[NQ], r3[NQ];
         ldrow<NQ>(w1b + m * NQ * XP, r1);
         ldrow<NQ>(w3a + m * XP, r3);
@@ -621,7 +596,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
 
     // ------------------------------------------------ back to the dofs
     T ye[ND];
-    if constexpr (IDENT || BDX_X_NOBACK) {
+    if constexpr (IDENT) {
 #pragma unroll
       for (int i = 0; i < ND; ++i) ye[i] = sx[i];
     } else {
@@ -634,7 +609,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
         T o[ND];
 #pragma unroll
         for (int i = 0; i < ND; ++i) o[i] = 0;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
+BDX_PRAGMA_UNROLL(1)
         for (int q = 0; q < NQ; ++q) {
           T row[ND];
           ldrow<ND>(w2b + q * NQ * XP, row);
@@ -649,7 +624,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
       for (int i = 0; i < ND; ++i) ye[i] = 0;
       if (a < ND && b < ND) {
         const T* __restrict__ pcb = s_tab + S::OFF_PC + b * XP;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL)
+BDX_PRAGMA_UNROLL(1)
         for (int q = 0; q < NQ; ++q) {
           T row[ND];
           ldrow<ND>(w1a + q * XP, row);
@@ -689,7 +664,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL)
 #pragma unroll
       for (int k = 0; k < NOUT; ++k) {
         const int m = o_meta[k];
-        if (BDX_X_NOOUT || !(m & kValid)) continue;
+        if (!(m & kValid)) continue;
         const int pl = (m >> 8) & 15, rem = m >> 12;
         T v = s_w2[o_src[k][0] & 0xffff] + s_w2[o_src[k][0] >> 16] +
               s_w2[o_src[k][1] & 0xffff] + s_w2[o_src[k][1] >> 16];
@@ -900,9 +875,6 @@ inline int fused_set_rect(Fused2Args<T>& a, const int* rect) {
 // synchronisation, bitwise identical to S = 1 except for the order of the
 // p.Ap partial sums (one per work item).
 //   mode argument of the apply entry points: kind | (S << 8), S = 0 -> 1.
-#ifndef BDX_SEG_WHOLE_ROUNDS
-#define BDX_SEG_WHOLE_ROUNDS 0  // A/B switch: the round-1 whole-round model
-#endif
 inline int fused_choose_segments(int tiles, int ncx, int resident) {
   if (tiles <= 0 || ncx <= 1 || resident <= 0) return 1;
   int best = 1;
@@ -915,13 +887,8 @@ inline int fused_choose_segments(int tiles, int ncx, int resident) {
     // (whole-round model vs this one, same box: fused5 Q3 6 -> 3 segments
     // 61.0 -> 61.7 GDoF/s, Q6 1 -> 2 segments 53.5 -> 54.3, fused3
     // x-trilinear Q6 1 -> 2 28.8 -> 29.8; profiles/r2_segments.md)
-#if BDX_SEG_WHOLE_ROUNDS
-    const double rounds = static_cast<double>((static_cast<int64_t>(tiles) * segs + resident - 1) /
-                                              resident);
-#else
     const double rounds =
         static_cast<double>(static_cast<int64_t>(tiles) * segs) / resident + 0.5;
-#endif
     // per work item: its layers, the redundant layer, and ~1 layer of
     // unpipelined prologue
     const double cost = rounds * (len + (S > 1 ? 2.0 : 1.0));

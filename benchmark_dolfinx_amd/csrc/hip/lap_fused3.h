@@ -20,83 +20,32 @@
 #pragma once
 #include "lap_fused2.h"
 
-#ifndef BDX_MUNROLL3
-#define BDX_MUNROLL3 2
-#endif
-// unroll of the per-quadrature-point x/F loop (full unroll hoists 2*ND*NQ
-// uniform table values into SGPRs, which spills beyond NQ = 5)
-// timing experiments (WRONG numerics): drop one stage / the intra-cell barriers
-#ifndef BDX_X3_NOFZ
-#define BDX_X3_NOFZ 0
-#endif
-#ifndef BDX_X3_NOFY
-#define BDX_X3_NOFY 0
-#endif
-#ifndef BDX_X3_NOXF
-#define BDX_X3_NOXF 0
-#endif
-#ifndef BDX_X3_NOBY
-#define BDX_X3_NOBY 0
-#endif
-#ifndef BDX_X3_NOBZ
-#define BDX_X3_NOBZ 0
-#endif
-#ifndef BDX_X3_NOSYNC
-#define BDX_X3_NOSYNC 0
-#endif
-// BDX_F3_LAUNDER: per-layer re-materialisation of the gather (bit 1) and
-// staging (bit 2) descriptors (see BDX_F5_LAUNDER in lap_fused5.h)
-#ifndef BDX_F3_LAUNDER
-#define BDX_F3_LAUNDER 3
-#endif
-#ifndef BDX_F3_STAGE_FIRST
-#define BDX_F3_STAGE_FIRST 1
-#endif
-#ifndef BDX_F3_ORECOMP
-#define BDX_F3_ORECOMP 1
-#endif
-// x-trilinear instances recompute the output descriptors as well (A/B switch)
-#ifndef BDX_F3_XORECOMP
-#define BDX_F3_XORECOMP 0
-#endif
-#ifndef BDX_F3_GQUNROLL
-#define BDX_F3_GQUNROLL 1
-#endif
+// Unroll of the per-quadrature-point x/F loop.  Parallelepiped instances:
+// full unroll up to NQ = 5, 2-way beyond (full unroll hoists 2*ND*NQ uniform
+// table values into SGPRs, which spills beyond NQ = 5).  General-geometry
+// instances (AFF = 0; FP32 only up to NQ = 5) and the x-trilinear FP64
+// instances (AFF = 2) keep the loop rolled, so the per-point geometry of one
+// point at a time is live, not NQ: general Q3 18.5 -> 21.4 GDoF/s (with 3
+// waves, below), x-trilinear Q3 25.0 -> 26.2, Q6 neutral; FP32 at NQ > 5
+// keeps the 2-way unroll (Q6 34.4 vs 33.9).  profiles/r2_launder.md,
+// r2_xtrilinear.md.
 template <int NQ> struct QUnroll3 { static constexpr int value = NQ <= 5 ? NQ : 2; };
-// general-geometry instances: BDX_F3_GQUNROLL > 0 overrides the x-loop unroll
-// (rolled: the per-point geometry of one point at a time is live, not NQ)
-// (FP32 at NQ > 5 keeps the 2-way unroll: 34.4 vs 33.9 GDoF/s at Q6)
-// x-trilinear FP64 instances (AFF = 2): BDX_F3_XQUNROLL > 0 overrides the
-// unroll.  Rolled (1) measured Q3 25.0 -> 26.2 GDoF/s, Q6 neutral (29.0 both);
-// FP32 keeps the default (Q6 46.2 vs 46.1 rolled), profiles/r2_xtrilinear.md
-#ifndef BDX_F3_XQUNROLL
-#define BDX_F3_XQUNROLL 1
-#endif
 template <typename T, int NQ, int AFF> struct QUnroll3G {
-  static constexpr bool on = !AFF && BDX_F3_GQUNROLL > 0 && (sizeof(T) == 8 || NQ <= 5);
-  static constexpr int value = on ? BDX_F3_GQUNROLL
-                               : (AFF == 2 && BDX_F3_XQUNROLL > 0 && sizeof(T) == 8) ? BDX_F3_XQUNROLL
-                                                                   : QUnroll3<NQ>::value;
+  static constexpr bool rolled =
+      (AFF == 0 && (sizeof(T) == 8 || NQ <= 5)) || (AFF == 2 && sizeof(T) == 8);
+  static constexpr int value = rolled ? 1 : QUnroll3<NQ>::value;
 };
-// Waves per SIMD the general (trilinear, AFF = 0) instances are compiled for.
-// With the fully unrolled per-point x loop the NQ = 5 instance needed ~250
-// VGPRs and 3 waves spilled 159 dwords; with the loop rolled
-// (BDX_F3_GQUNROLL = 1) it is 175 VGPRs at 2 waves and fits 3 waves with an
-// 8-dword spill: Q3 general 18.5 -> 21.4 GDoF/s (same box, job_r2af.sh).
-// LDS caps the P >= 4 instances at 2 workgroups per CU anyway, and there the
-// compiler keeps its 2-wave allocation (no spill).
-#ifndef BDX_FUSED3_GWAVES
-#define BDX_FUSED3_GWAVES 3
-#endif
-// AFF = 2 (x-trilinear cells, see the geometry block) carries ~10 geometry
-// registers instead of the 15-value trilinear set
-#ifndef BDX_FUSED3_XWAVES
-#define BDX_FUSED3_XWAVES 3
-#endif
+// Waves per SIMD the instances are compiled for.  General (AFF = 0) and
+// x-trilinear (AFF = 2) cells: 3.  With the rolled per-point x loop the NQ = 5
+// general instance is 175 VGPRs at 2 waves and fits 3 waves with an 8-dword
+// spill (Q3 general 18.5 -> 21.4 GDoF/s, job_r2af.sh).  LDS caps the P >= 4
+// instances at 2 workgroups per CU anyway, and there the compiler keeps its
+// 2-wave allocation (no spill).
 template <int NQ, int AFF> struct Fused3Waves {
-  static constexpr int value =
-      AFF == 1 ? FusedWaves<NQ>::value : (AFF == 2 ? BDX_FUSED3_XWAVES : BDX_FUSED3_GWAVES);
+  static constexpr int value = AFF == 1 ? FusedWaves<NQ>::value : 3;
 };
+// The gather and staging descriptors are re-materialised every layer through
+// an empty asm (the descriptor laundering of lap_fused5.h).
 
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
@@ -302,7 +251,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
   // (frees 4 NOUT VGPRs: the Q6 general CG instance spilled 34 dwords with them
   // resident; same-box Q6 general 18.8 -> 22.0 GDoF/s, while Q3 general, which
   // did not spill, drops 18.2 -> 14.0 with the recomputation)
-  constexpr bool ORECOMP = BDX_F3_ORECOMP && (AFF == 0 || (AFF == 2 && BDX_F3_XORECOMP)) && NQ >= 7;
+  constexpr bool ORECOMP = AFF == 0 && NQ >= 7;
   int o_src[ORECOMP ? 1 : NOUT][2], o_off[ORECOMP ? 1 : NOUT], o_meta[ORECOMP ? 1 : NOUT];
   if constexpr (!ORECOMP) {
 #pragma unroll
@@ -397,7 +346,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
-      if (!BDX_X_NOSTAGE && !last && (st_meta[k] & kValid)) {
+      if (!last && (st_meta[k] & kValid)) {
         pf_r[k] = A.u[lnext + st_goff[k]];
         if constexpr (MODE == kFusedCG) {
           pf_p[k] = A.pold[lnext + st_goff[k]];
@@ -425,7 +374,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      } else if constexpr (!BDX_X3_NOSYNC) {
+      } else {
         __syncthreads();
       }
     };
@@ -439,7 +388,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
 
     // ------------------------------------------------ front z: (B_z u, Dd_z u)
     // lanes (c, j = a < ND, qz = b): rows over the cell's x dofs i
-    if (!BDX_X3_NOFZ && lane_on && a < ND) {
+    if (lane_on && a < ND) {
       const T* __restrict__ br = s_tab + OFF_BR + b * NP;
       const T* __restrict__ dr = s_tab + OFF_DR + b * NP;
       T ob[ND], od[ND];
@@ -469,8 +418,8 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
     {
       const T* __restrict__ bra = s_tab + OFF_BR + a * NP;
       const T* __restrict__ dra = s_tab + OFF_DR + a * NP;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
-      for (int j = 0; j < (BDX_X3_NOFY ? 0 : ND); ++j) {
+BDX_PRAGMA_UNROLL(2)
+      for (int j = 0; j < ND; ++j) {
         T rb[ND], rd[ND];
         const int o = offA(c, j, b);
         ldrow<ND>(W0 + o, rb);
@@ -573,7 +522,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
 #pragma unroll
     for (int i = 0; i < ND; ++i) a1[i] = a2[i] = a3[i] = T(0);
 BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
-    for (int q = 0; q < (BDX_X3_NOXF ? 1 : NQ); ++q) {
+    for (int q = 0; q < NQ; ++q) {
       T gxq = 0, gyq = 0, gzq = 0;
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
@@ -641,7 +590,7 @@ BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
       if (lane_on && a < ND) {
         const T* bcj = s_tab + OFF_BC + a * XP;
         const T* dcj = s_tab + OFF_DC + a * XP;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
+BDX_PRAGMA_UNROLL(2)
         for (int qy = 0; qy < NQ; ++qy) {
           T r1[ND], r2[ND];
           ldrow<ND>(W0 + offA(c, qy, b), r1);
@@ -661,7 +610,7 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
       for (int i = 0; i < ND; ++i) c3[i] = T(0);
       if (lane_on && a < ND) {
         const T* bcj = s_tab + OFF_BC + a * XP;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
+BDX_PRAGMA_UNROLL(2)
         for (int qy = 0; qy < NQ; ++qy) {
           T r3[ND];
           ldrow<ND>(W1 + offA(c, qy, b), r3);
@@ -690,8 +639,8 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
       if (lane_on && a < ND) {
         const T* bcj = s_tab + OFF_BC + a * XP;
         const T* dcj = s_tab + OFF_DC + a * XP;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
-        for (int qy = 0; qy < (BDX_X3_NOBY ? 0 : NQ); ++qy) {
+BDX_PRAGMA_UNROLL(2)
+        for (int qy = 0; qy < NQ; ++qy) {
           const int o = offA(c, qy, b);
           T r1[ND], r2[ND], r3[ND];
           ldrow<ND>(W0 + o, r1);
@@ -721,8 +670,8 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
     if (lane_on && a < ND && b < ND) {
       const T* bck = s_tab + OFF_BC + b * XP;
       const T* dck = s_tab + OFF_DC + b * XP;
-BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
-      for (int qz = 0; qz < (BDX_X3_NOBZ ? 0 : NQ); ++qz) {
+BDX_PRAGMA_UNROLL(2)
+      for (int qz = 0; qz < NQ; ++qz) {
         const int o = offA(c, a, qz);
         T r1[ND], r3[ND];
         ldrow<ND>(W0 + o, r1);
@@ -766,14 +715,13 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
             asm volatile("" : "+v"(e));  // recompute here, not hoisted out of the march
             out_desc(e, os0, os1, ooff, m);
           } else {
-            if (BDX_F3_LAUNDER & 1)
-              asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
+            asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
             os0 = o_src[k][0];
             os1 = o_src[k][1];
             ooff = o_off[k];
             m = o_meta[k];
           }
-          if (BDX_X_NOOUT || !(m & kValid)) continue;
+          if (!(m & kValid)) continue;
           const int pl = (m >> 8) & 15, rem = m >> 12;
           T v = s_wa[os0 & 0xffff] + s_wa[os0 >> 16] + s_wa[os1 & 0xffff] + s_wa[os1 >> 16];
           if (pl == 0) v += s_c[cur][rem];
@@ -803,10 +751,8 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
     auto do_stage = [&]() __attribute__((always_inline)) {
       // ------------------------------------------------ stage the next layer
       if (!last) {
-        if (BDX_F3_LAUNDER & 2) {
-  #pragma unroll
-          for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
-        }
+        #pragma unroll
+        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
         T* __restrict__ un = s_u[nxt];
   #pragma unroll
         for (int k = 0; k < NCP; ++k)
@@ -859,16 +805,11 @@ BDX_PRAGMA_UNROLL(BDX_MUNROLL3)
         }
       }
     };
-    // BDX_F3_STAGE_FIRST: consume the prefetch before the gather stores,
-    // behind one explicit vmcnt(0) (see BDX_F5_STAGE_FIRST)
-    if constexpr (BDX_F3_STAGE_FIRST) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      do_stage();
-      do_gather();
-    } else {
-      do_gather();
-      do_stage();
-    }
+    // Consume the prefetch before the gather stores,
+    // behind one explicit vmcnt(0) (as in lap_fused5.h)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    do_stage();
+    do_gather();
     kc_cur = kc_nxt;
   }
   if constexpr (MODE == kFusedCG) {

@@ -28,53 +28,15 @@
 
 #include "lap_fused2.h"
 
-#ifndef BDX_F4_TY
-#define BDX_F4_TY 4
-#endif
-#ifndef BDX_F4_TZ
-#define BDX_F4_TZ 4
-#endif
-// BDX_F4_LAUNDER: re-materialise the per-thread gather (bit 1) / staging
-// (bit 2) descriptors every layer through an empty asm, so the compiler
-// cannot hoist their unpacked fields and flag masks out of the x-march
-// (hoisted, the SGPR masks spill to VGPR lanes: v_readlane per use).
-// Off by default: it removes the loop's 111 v_readlane and 19 VGPRs, but
-// fused4 is LDS-limited to 3 workgroups per CU and a same-box A/B was
-// neutral (52.3 vs 52.6 GDoF/s, profiles/r2_launder.md)
-#ifndef BDX_F4_LAUNDER
-#define BDX_F4_LAUNDER 0
-#endif
-#ifndef BDX_F4_WAVES
-#define BDX_F4_WAVES 3
-#endif
-// Timing-only phase drops for A/B attribution (wrong numerics when nonzero):
-// 1 = MFMA core, 2 = gather + write-out, 4 = next-layer global loads,
-// 8 = x contraction + geometry, 16 = the two workgroup barriers per layer.
-#ifndef BDX_F4_RP
-#define BDX_F4_RP 4
-#endif
-#ifndef BDX_F4_P1
-#define BDX_F4_P1 17
-#endif
-#ifndef BDX_F4_PC
-#define BDX_F4_PC 72
-#endif
-#ifndef BDX_F4_NOSKIP
-#define BDX_F4_NOSKIP 0
-#endif
-#ifndef BDX_F4_DROP
-#define BDX_F4_DROP 0
-#endif
-// 1: the per-lane x-factor rows live in LDS (read per layer, 32 fewer VGPRs)
-// instead of registers
-#ifndef BDX_F4_XLDS
-#define BDX_F4_XLDS 1
-#endif
-// 1: the gather-source descriptors (4 packed LDS offsets per output slot)
-// live in LDS instead of registers
-#ifndef BDX_F4_OLDS
-#define BDX_F4_OLDS 1
-#endif
+// Fixed design choices (same-box A/Bs in profiles/r1_kernel_ab.md,
+// r2_launder.md, r2_fused4_attribution.md):
+//  * 4 x 4 cell tile, 3 waves/SIMD (LDS-limited to 3 workgroups per CU);
+//  * the per-lane x-factor rows and the gather-source descriptors (4 packed
+//    LDS offsets per output slot) live in LDS, not registers (32 + 16 VGPRs);
+//  * no descriptor laundering (it removes 111 v_readlane and 19 VGPRs, but
+//    the kernel is LDS-limited and the A/B was neutral, 52.3 vs 52.6 GDoF/s).
+
+constexpr int kF4TY = 4, kF4TZ = 4;  // cell tile
 
 typedef double bdx_f64x4 __attribute__((ext_vector_type(4)));
 typedef double bdx_f64x2 __attribute__((ext_vector_type(2)));
@@ -97,8 +59,8 @@ __device__ __forceinline__ double f4_mat(const double* tab, int id, int r, int c
 }
 
 // fused4: MFMA (y, z) Kronecker core on parallelepiped Q3 cells, x-marching CG fusion.
-template <int TY, int TZ, int MODE, int DEPTH>
-__global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
+template <int TY, int TZ, int MODE>
+__global__ void __launch_bounds__(TY * TZ * 16, 3)
     lap_fused4_kernel(Fused2Args<double> A, FusedTables<double> tb) {
   using T = double;
   constexpr int ND = 4, P = 3;
@@ -117,7 +79,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   // (b64: 2 x 32 lanes, 64 banks; scripts/lds_bank_f4.py): 135 LDS cycles per
   // workgroup layer vs 257 for the earlier odd pitches (5, 21, 85), ideal 112; the
   // same-box A/B is neutral (38.50 vs 38.47 GDoF/s): LDS is not the limiter
-  constexpr int RP = BDX_F4_RP, P1 = BDX_F4_P1, PC = BDX_F4_PC;
+  constexpr int RP = 4, P1 = 17, PC = 72;
   constexpr int EB = CELLS * PC;
   constexpr int ZSLOT = EB;
   static_assert(ZSLOT < 32768, "16-bit LDS source offsets");
@@ -130,12 +92,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   __shared__ T s_e[EB + 1];
   __shared__ T s_X[2][2 * NV];
   __shared__ T s_kc[2][CELLS];  // per-cell coefficient, double buffered
-#if BDX_F4_XLDS
   __shared__ __attribute__((aligned(16))) T s_Xr[4 * 4 * ND];  // [m][xi][l]
-#endif
-#if BDX_F4_OLDS
   __shared__ __attribute__((aligned(8))) int s_osrc[NOUT][NT][2];
-#endif
   __shared__ double s_red[16];
 
   const int tid = threadIdx.x;
@@ -181,16 +139,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   const int cy = c / TZ, cz = c % TZ;
   const bool cell_on = (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
   // this lane's rows X[xi][.] of the four x factors
-#if BDX_F4_XLDS
   if (tid < 64) s_Xr[tid] = f4_mat(tab, tid >> 4, (tid >> 2) & 3, tid & 3);
   const T* __restrict__ XrL = s_Xr + xi * ND;
-#else
-  T Xr[4][ND];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int l = 0; l < ND; ++l) Xr[m][l] = f4_mat(tab, m, xi, l);
-#endif
 
   T beta = T(0), xalpha = T(0);
   const bool xupd = MODE == kFusedCG && A.xa_num >= 0;
@@ -260,18 +210,12 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     }
   }
   // ---- per-thread output descriptors (planes 0..P of a layer)
-#if BDX_F4_OLDS
   int(*o_src)[NT][2] = s_osrc;
-#define BDX_F4_OSRC(k, h) o_src[k][tid][h]
-#else
-  int o_src[NOUT][2];
-#define BDX_F4_OSRC(k, h) o_src[k][h]
-#endif
   int o_off[NOUT], o_meta[NOUT];
 #pragma unroll
   for (int k = 0; k < NOUT; ++k) {
     const int e = tid + k * NT;
-    BDX_F4_OSRC(k, 0) = BDX_F4_OSRC(k, 1) = ZSLOT | (ZSLOT << 16);
+    o_src[k][tid][0] = o_src[k][tid][1] = ZSLOT | (ZSLOT << 16);
     o_off[k] = 0;
     o_meta[k] = 0;
     if (e < ND * PL) {
@@ -287,8 +231,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
         for (int ccy = cyl; ccy <= cyh; ++ccy)
           for (int ccz = czl; ccz <= czh; ++ccz)
             src[ns++] = (ccy * TZ + ccz) * PC + (ly - ccy * P) * P1 + (lz - ccz * P) * RP + pl;
-        BDX_F4_OSRC(k, 0) = src[0] | (src[1] << 16);
-        BDX_F4_OSRC(k, 1) = src[2] | (src[3] << 16);
+        o_src[k][tid][0] = src[0] | (src[1] << 16);
+        o_src[k][tid][1] = src[2] | (src[3] << 16);
         const int gy = y0 + ly, gz = z0 + lz;
         const bool iy = ly < oy, iz = lz < oz;
         int kind, off;
@@ -366,17 +310,15 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
   // waitcnt pass carries the Xr loads as pending around the loop and makes
   // their uses inside the MFMA core wait for each layer's prefetch batch.
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  // Prefetch of layer cx + DEPTH (its planes 1..P, vertex plane cx + DEPTH + 1
-  // and cell coefficient) into one register set.  Every load is issued
-  // unconditionally (past the segment it re-reads layer 0, unused), so each
-  // layer issues the same number of loads and the wait for a set can be a
-  // counted vmcnt that leaves the younger set in flight.
+  // Prefetch of layer cx + 1 (its planes 1..P, vertex plane cx + 2 and cell
+  // coefficient) into one register set (a second set, two layers ahead,
+  // measured 1.2-1.5 % slower: it costs occupancy headroom).  Every load is
+  // issued unconditionally (past the segment it re-reads layer 0, unused).
   struct PF {
     T r[NPF], p[NPF], x[NPF];
     T v[NPV];
     T kc;
   };
-  constexpr int NLD = (MODE == kFusedCG ? 3 : 1) * NPF + NPV + 1;  // loads per set
   const T* __restrict__ kcp = A.kc ? A.kc : A.xv;
   auto issue = [&](PF& f, int cl) __attribute__((always_inline)) {
     const bool in = cl < cend;
@@ -386,13 +328,11 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       f.r[k] = T(0);
       f.p[k] = T(0);
       f.x[k] = T(0);
-      if constexpr ((BDX_F4_DROP & 4) == 0) {
-        if (BDX_OOB(lpf + st_goff[k], A.vsize, "f4 prefetch")) continue;
-        f.r[k] = ld_stream(A.u + lpf + st_goff[k]);
-        if constexpr (MODE == kFusedCG) {
-          f.p[k] = ld_stream(A.pold + lpf + st_goff[k]);
-          f.x[k] = ld_stream(A.x + lpf + st_goff[k]);
-        }
+      if (BDX_OOB(lpf + st_goff[k], A.vsize, "f4 prefetch")) continue;
+      f.r[k] = ld_stream(A.u + lpf + st_goff[k]);
+      if constexpr (MODE == kFusedCG) {
+        f.p[k] = ld_stream(A.pold + lpf + st_goff[k]);
+        f.x[k] = ld_stream(A.x + lpf + st_goff[k]);
       }
     }
     const int64_t lv = (in && cl + 1 <= ncx) ? static_cast<int64_t>(cl + 1) * A.vps : 0;
@@ -400,25 +340,16 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     for (int k = 0; k < NPV; ++k) f.v[k] = A.xv[lv + (v_off[k] >= 0 ? v_off[k] : 0)];
     f.kc = kcp[(A.kc && in) ? static_cast<int64_t>(cl) * kc_ps + kc_cell : 0];
   };
-  // s_waitcnt vmcnt(n), expcnt / lgkmcnt untouched (gfx9 encoding)
-  constexpr int kWaitNewest = 0x0F70 | (NLD & 15) | ((NLD >> 4) << 14);
-
-  auto layer = [&](int cx, PF& pfc, PF& pfn) __attribute__((always_inline)) {
+  auto layer = [&](int cx, PF& pfc) __attribute__((always_inline)) {
     const int cur = (cx - cbeg) & 1, nxt = cur ^ 1;
     const bool last = (cx == cend - 1);   // end of this segment
     const bool glast = (cx == ncx - 1);   // end of the march
     const bool red = (cx < sa);           // redundant layer: carry only
-    if constexpr ((BDX_F4_DROP & 16) == 0) __syncthreads();
+    __syncthreads();
 
-    // ---- prefetch: DEPTH 1 loads layer cx+1 into pfc (used at the end of
-    // this layer); DEPTH 2 loads layer cx+2 into pfn while pfc (layer cx+1,
-    // issued one layer ago) is still landing
+    // ---- prefetch: layer cx+1 into pfc (used at the end of this layer)
     const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
-    if constexpr (DEPTH == 1) {
-      issue(pfc, cx + 1);
-    } else {
-      issue(pfn, cx + 2);
-    }
+    issue(pfc, cx + 1);
     T(&pf_r)[NPF] = pfc.r;
     T(&pf_p)[NPF] = pfc.p;
     T(&pf_x)[NPF] = pfc.x;
@@ -429,14 +360,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
 
     // ------------------------------------------------ geometry (constant J)
     T G00, G01, G02, G11, G12, G22;
-    if constexpr ((BDX_F4_DROP & 8) != 0) {
-      G00 = sX[c];
-      G01 = sX[c + 1];
-      G02 = sX[c + 2];
-      G11 = sX[c + 3];
-      G12 = sX[c + 4];
-      G22 = sX[c + 5];
-    } else {
+    {
       const T* X0 = sX;
       const T* X1 = sX + NV;
       const int v00 = (cy * (TZ + 1) + cz) * 3, v01 = v00 + 3;
@@ -476,11 +400,6 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       for (int j = 0; j < ND; ++j) uu[l][j] = ub[l * PLP + j * DZP];
     bdx_f64x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
     auto block = [&](int t, const T (&V)[ND], T gt) {
-      if constexpr ((BDX_F4_DROP & 1) != 0) {
-        acc0[t & 3] += V[0] + V[1];
-        acc1[t & 3] += V[2] + V[3] + gt;
-        return;
-      }
       const bdx_f64x2 a01 = *reinterpret_cast<const bdx_f64x2*>(s_Al + (2 * t) * 128);
       const bdx_f64x2 a23 = *reinterpret_cast<const bdx_f64x2*>(s_Al + (2 * t + 1) * 128);
       acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a01[0], gt * V[0], acc0, 0, 0, 0);
@@ -489,18 +408,9 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a23[1], gt * V[3], acc1, 0, 0, 0);
     };
     auto xcontract = [&](int m, T (&V)[ND]) {
-      if constexpr ((BDX_F4_DROP & 8) != 0) {
-#pragma unroll
-        for (int j = 0; j < ND; ++j) V[j] = uu[m][j];
-        return;
-      }
-#if BDX_F4_XLDS
       const bdx_f64x2 x01 = *reinterpret_cast<const bdx_f64x2*>(XrL + m * 16);
       const bdx_f64x2 x23 = *reinterpret_cast<const bdx_f64x2*>(XrL + m * 16 + 2);
       const T xr[ND] = {x01[0], x01[1], x23[0], x23[1]};
-#else
-      const T(&xr)[ND] = Xr[m];
-#endif
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
         T s = T(0);
@@ -514,12 +424,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       // G01 = G02 = G12 = 0 exactly; when that holds for every cell of the
       // wave the five mixed blocks contribute exact zeros to the MFMA
       // accumulators and are skipped (wave-uniform branch, bit-identical
-      // result).  BDX_F4_NOSKIP=1 always runs them (A/B and documentation).
-#if BDX_F4_NOSKIP
-      const bool mixed = true;
-#else
+      // result).
       const bool mixed = __any((G01 != T(0)) || (G02 != T(0)) || (G12 != T(0)));
-#endif
       T V[ND];
       xcontract(1, V);  // K1 along x
       block(0, V, G00);
@@ -550,7 +456,7 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
 #pragma unroll
       for (int r = 0; r < ND; ++r) eo[r * P1] = cell_on ? ye[r] : T(0);
     }
-    if constexpr ((BDX_F4_DROP & 16) == 0) __syncthreads();
+    __syncthreads();
 
     // ------------------------------------------------ stage the next layer (LDS)
     // The prefetched values go to LDS before any global store of this layer
@@ -559,15 +465,8 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     // writes) drain while the next layer computes.  The wait is explicit and
     // unconditional (vmcnt(0) only; gfx9 encoding) so the waitcnt pass sees
     // no prefetch register pending on any path after this point.
-    if constexpr (DEPTH == 1)
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-    else
-      __builtin_amdgcn_s_waitcnt(kWaitNewest);  // pfc landed, pfn in flight
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // pfc landed
     if (!last) {
-      if (BDX_F4_LAUNDER & 2) {
-#pragma unroll
-        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
-      }
       T* __restrict__ un = s_u[nxt];
 #pragma unroll
       for (int k = 0; k < NCP; ++k)
@@ -610,20 +509,16 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
     }
 
     // ------------------------------------------------ gather-sum and write out
-    if constexpr ((BDX_F4_DROP & 2) == 0) {
+    {
       const int64_t lbase = static_cast<int64_t>(cx) * P;
       T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
                                   A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
-      if (BDX_F4_LAUNDER & 1) {
-#pragma unroll
-        for (int k = 0; k < NOUT; ++k) asm volatile("" : "+v"(o_off[k]), "+v"(o_meta[k]));
-      }
 #pragma unroll
       for (int k = 0; k < NOUT; ++k) {
         const int m = o_meta[k];
         if (!(m & kValid)) continue;
         const int pl = (m >> 8) & 15, rem = m >> 12;
-        const int os0 = BDX_F4_OSRC(k, 0), os1 = BDX_F4_OSRC(k, 1);
+        const int os0 = o_src[k][tid][0], os1 = o_src[k][tid][1];
         BDX_DASSERT((os0 & 0xffff) <= ZSLOT && (os0 >> 16) <= ZSLOT && (os1 & 0xffff) <= ZSLOT &&
                     (os1 >> 16) <= ZSLOT && rem < PL);
         T v = s_e[os0 & 0xffff] + s_e[os0 >> 16] + s_e[os1 & 0xffff] + s_e[os1 >> 16];
@@ -674,18 +569,18 @@ __global__ void __launch_bounds__(TY * TZ * 16, BDX_F4_WAVES)
       }
     }
   };
+  // two layers per trip, alternating register sets (the rolled loop with one
+  // set spills 8 dwords in the CG instance)
   PF pfa, pfb;
-  if constexpr (DEPTH == 2) issue(pfa, cbeg + 1);
   for (int cx = cbeg; cx < cend; cx += 2) {
-    layer(cx, pfa, pfb);
-    if (cx + 1 < cend) layer(cx + 1, pfb, pfa);
+    layer(cx, pfa);
+    if (cx + 1 < cend) layer(cx + 1, pfb);
   }
   if constexpr (MODE == kFusedCG) {
     const double t = block_sum(pap, s_red);
     // indexed by (tile, segment): invariant under any launch split
     if (tid == 0) A.partials[(ty * A.ntz + tz) * A.nseg + seg] = t;
   }
-#undef BDX_F4_OSRC
 }
 
 // 1D matrices of the quadrature rule (host, double): M1 = B^T W B,
@@ -710,26 +605,11 @@ inline int pack_tables4(int nd, int nq, const double* phi0, const double* Dd, co
   return kFusedTabMax;
 }
 
-// Prefetch depth of the x-march (layers in flight ahead of the one being
-// computed): BDX_F4_DEPTH=1|2 at run time (A/B), default 1 (depth 2 measured
-// 1.2-1.5 % slower in an interleaved same-box A/B, Q3 300 M: 45.4/45.5 vs
-// 46.1/46.1 GDoF/s; the second register set costs occupancy headroom).
-inline int fused4_depth() {
-  static const int d = [] {
-    const char* e = std::getenv("BDX_F4_DEPTH");
-    return (e && std::atoi(e) == 2) ? 2 : 1;
-  }();
-  return d;
-}
-
 template <int MODE>
 int launch_fused4(const Fused2Args<double>& a, const FusedTables<double>& tb, hipStream_t st) {
-  constexpr int TY = BDX_F4_TY, TZ = BDX_F4_TZ;
+  constexpr int TY = kF4TY, TZ = kF4TZ;
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
-  if (fused4_depth() == 1)
-    lap_fused4_kernel<TY, TZ, MODE, 1><<<nblk, TY * TZ * 16, 0, st>>>(a, tb);
-  else
-    lap_fused4_kernel<TY, TZ, MODE, 2><<<nblk, TY * TZ * 16, 0, st>>>(a, tb);
+  lap_fused4_kernel<TY, TZ, MODE><<<nblk, TY * TZ * 16, 0, st>>>(a, tb);
   return static_cast<int>(hipGetLastError());
 }

@@ -50,26 +50,20 @@ extern "C" int bdx_fused4_tables_f64(int nd, int nq, const double* phi0, const d
 
 // Cell tile (TY, TZ) of the fused4 instance, for the host-side launch geometry.
 extern "C" int bdx_fused4_tile(int* ty, int* tz) {
-  *ty = BDX_F4_TY;
-  *tz = BDX_F4_TZ;
+  *ty = kF4TY;
+  *tz = kF4TZ;
   return 0;
 }
-
-// Timing-only phase drops compiled into this TU (0 in a valid build).
-extern "C" int bdx_drop_flags_f4() { return BDX_F4_DROP; }
 
 // x segments per tile for a launch of `tiles` tiles marching `ncx` layers
 // (fused_choose_segments with this kernel's resident workgroups).
 extern "C" int bdx_fused4_segments(int tiles, int ncx) {
-  constexpr int TY = BDX_F4_TY, TZ = BDX_F4_TZ;
+  constexpr int TY = kF4TY, TZ = kF4TZ;
   int per_cu = 0, dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      (fused4_depth() == 1
-           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                 &per_cu, lap_fused4_kernel<TY, TZ, kFusedCG, 1>, TY * TZ * 16, 0)
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                 &per_cu, lap_fused4_kernel<TY, TZ, kFusedCG, 2>, TY * TZ * 16, 0)) != hipSuccess)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, lap_fused4_kernel<TY, TZ, kFusedCG>, TY * TZ * 16, 0) != hipSuccess)
     return 1;
   return fused_choose_segments(tiles, ncx, per_cu * cus);
 }

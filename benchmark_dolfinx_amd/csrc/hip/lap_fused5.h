@@ -43,108 +43,52 @@
 
 #include "lap_fused2.h"
 
-#ifndef BDX_F5_WAVES
-#define BDX_F5_WAVES 2
-#endif
-// Timing-only phase drops for A/B attribution (wrong numerics when nonzero):
-// 1 = z/y passes, 2 = gather + write-out, 4 = next-layer global loads.
-#ifndef BDX_F5_DROP
-#define BDX_F5_DROP 0
-#endif
+// Resident waves per SIMD the kernel is compiled for (__launch_bounds__):
+// the FP64 Q6 CG instance is 170 VGPRs, so 2; a 3-wave build spills and
+// measured 9 % slower (profiles/r2_launder.md).
+constexpr int kF5Waves = 2;
 
 // table layout: M, K, C, C^T as 8 x 8 row-major blocks, then the even-odd
 // forms of M and K (4 x 4 blocks at kF5EO + 32 id: E, then O at + 16)
 constexpr int kF5Stride = 8;
 constexpr int kF5EO = 4 * 64;
-// packed even-odd rows for FP32 (BDX_F5_PK): row a of id at kF5PK + 32 id +
-// 8 a holds (E[a][b], O[a][b]) pairs, b = 0..3 (odd nd: the middle column
-// E[a][nd/2] in the pair after the last full one, with O = 0)
-constexpr int kF5PK = kF5EO + 2 * 32;
-constexpr int kF5Tab = kF5PK + 2 * 32;
+constexpr int kF5Tab = kF5EO + 2 * 32;
 // Even-odd decomposition of the centrosymmetric M and K (M[i][j] =
 // M[nd-1-i][nd-1-j] for the symmetric GLL / Gauss rules; checked on the
 // host): out = M in costs ceil(nd/2) x ceil(nd/2) + floor(nd/2)^2 FMAs
 // instead of nd^2 (31 instead of 49 at nd = 7) and half the scalar table
-// loads.  BDX_F5_EO=0 keeps the plain row products (A/B).
-#ifndef BDX_F5_EO
-#define BDX_F5_EO 1
-#endif
-// passes that use it (bit 1 x, 2 z, 4 y) per precision: FP32 all (+11 % at
-// Q6 in a same-box A/B).  FP64 all passes spilled 10 dwords in the CG
-// instance before the descriptor laundering (BDX_F5_LAUNDER); with it the
-// instance is 188 VGPRs, spill-free, and all passes win (50.4 vs 49.9)
-#ifndef BDX_F5_EO_F32
-#define BDX_F5_EO_F32 7
-#endif
-#ifndef BDX_F5_EO_F64
-#define BDX_F5_EO_F64 7
-#endif
-// BDX_F5_LAUNDER: re-materialise the per-thread gather (bit 1) / staging
-// (bit 2) descriptors every layer through an empty asm, so the compiler
-// cannot hoist their unpacked fields and flag masks out of the x-march
-// (hoisted, they cost ~20 VGPRs and the SGPR masks spill to VGPR lanes)
-#ifndef BDX_F5_LAUNDER
-#define BDX_F5_LAUNDER 3
-#endif
-// BDX_F5_PK: packed-math (v_pk_fma_f32) even-odd products in the FP32
-// instances.  8 % fewer loop instructions (1406 -> 1295) but neutral in a
-// same-box A/B (Q6 FP32 91.2 vs 91.3 GDoF/s, profiles/r2_launder.md): the
-// FP32 kernel is not VALU-issue-bound, so the scalar form stays the default
-#ifndef BDX_F5_PK
-#define BDX_F5_PK 0
-#endif
-// BDX_F5_ZSPLIT: z pass of the 2-array instance writes zK back before
-// forming zM (fewer live registers at the pass's peak: Q6 FP64 CG instance
-// 188 -> 170 VGPRs; +0.9 % Q6 FP64, +0.6 % Q6 FP32 same box).  The 3-wave
-// builds it enables (164 VGPRs spill-free with even-odd on x/y) measured
-// slower: 50.2 vs 52.5 GDoF/s (profiles/r2_launder.md)
-// BDX_F5_STAGE_FIRST: consume the prefetch (LDS staging and the p / x
-// stores) before the gather's stores, behind one explicit vmcnt(0).  In the
-// other order the prefetch registers are read after the gather's divergent
-// stores, the waitcnt pass cannot count them, and every staging slot waits
-// with vmcnt(0), draining all stores issued before it.  Same box: Q3 +4.1 %,
-// Q6 FP64 +1.1 %, Q6 FP32 +2.8 % (profiles/r2_launder.md)
-#ifndef BDX_F5_STAGE_FIRST
-#define BDX_F5_STAGE_FIRST 1
-#endif
-#ifndef BDX_F5_ZSPLIT
-#define BDX_F5_ZSPLIT 1
-#endif
-#ifndef BDX_F5_LBASE
-#define BDX_F5_LBASE 1
-#endif
+// loads.  Used on all three passes in both precisions (FP32 +11 % at Q6,
+// FP64 spill-free at 188 VGPRs with the descriptor laundering below).
+//
+// Register-pressure measures that the production kernel relies on (each an
+// A/B on the box, profiles/r2_launder.md):
+//  * descriptor laundering: the per-thread gather / staging descriptors are
+//    re-materialised every layer through an empty asm, so the compiler cannot
+//    hoist their unpacked fields and flag masks out of the x-march (hoisted,
+//    they cost ~20 VGPRs and the SGPR masks spill to VGPR lanes);
+//  * one laundered table base pointer per matrix row, rows addressed by a
+//    constant offset (folded into the scalar load's immediate);
+//  * the z pass writes zK back before forming zM (one output row live, not
+//    two: Q6 FP64 188 -> 170 VGPRs, +0.9 %);
+//  * the prefetch is consumed (LDS staging, p / x stores) before the
+//    gather's stores, behind one explicit vmcnt(0) (Q3 +4.1 %, Q6 +1.1 %).
 static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
 
 // cells per wave and (y, z) tile per degree; NARR = 4 (sheared cells) keeps
-// the 2 x 2 tile at ND >= 6 (its per-wave buffers are twice as large)
-template <int ND, int NARR> struct F5Tile;
-#ifndef BDX_F5_TY4
-#define BDX_F5_TY4 4
-#endif
-#ifndef BDX_F5_TZ4
-#define BDX_F5_TZ4 4
-#endif
-template <> struct F5Tile<4, 2> { static constexpr int CPW = 4, TY = BDX_F5_TY4, TZ = BDX_F5_TZ4; };
-template <> struct F5Tile<4, 4> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
-template <int NARR> struct F5Tile<5, NARR> { static constexpr int CPW = 2, TY = 2, TZ = 4; };
-template <int NARR> struct F5Tile<6, NARR> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
-#ifndef BDX_F5_TY7
-#define BDX_F5_TY7 2
-#endif
-#ifndef BDX_F5_TZ7
-#define BDX_F5_TZ7 2
-#endif
-template <> struct F5Tile<7, 2> { static constexpr int CPW = 1, TY = BDX_F5_TY7, TZ = BDX_F5_TZ7; };
-template <> struct F5Tile<7, 4> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
-template <int NARR> struct F5Tile<8, NARR> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+// the 2 x 2 tile at ND >= 6 (its per-wave buffers are twice as large).
+// Tile shapes: same-box A/Bs of 4x4 vs 4x2 at ND = 4 and 2x2 vs 2x1 at
+// ND = 7 kept these (profiles/r2_fused5_evenodd.md).
+template <int ND> struct F5Tile;
+template <> struct F5Tile<4> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
+template <> struct F5Tile<5> { static constexpr int CPW = 2, TY = 2, TZ = 4; };
+template <> struct F5Tile<6> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+template <> struct F5Tile<7> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
+template <> struct F5Tile<8> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 
-// MFMA core (MF = 1, axis-aligned 2-array instance, one cell per wave):
-// per-wave buffer holds Kx u, Mx u (2 ND^3) and zM, zK (2 ND^3)
-template <typename T, int ND, int NARR, int MF = 0>
+template <typename T, int ND, int NARR>
 struct F5Shape {
   static constexpr int P = ND - 1;
-  static constexpr int CPW = F5Tile<ND, NARR>::CPW, TY = F5Tile<ND, NARR>::TY,
-                       TZ = F5Tile<ND, NARR>::TZ;
+  static constexpr int CPW = F5Tile<ND>::CPW, TY = F5Tile<ND>::TY, TZ = F5Tile<ND>::TZ;
   static constexpr int CELLS = TY * TZ;
   static_assert(CELLS % CPW == 0, "whole waves of cells");
   static constexpr int WAVES = CELLS / CPW;
@@ -157,43 +101,18 @@ struct F5Shape {
   // element vectors for the gather: E[cell][j][k][i]
   static constexpr int RP = ND, P1 = ND * ND, PC = ND * ND * ND;
   static constexpr int WB0 = NARR * ARR;
-  static constexpr int WB1 = WB0 > CPW * PC ? WB0 : CPW * PC;
-  static constexpr int WB = (MF && 4 * PC > WB1) ? 4 * PC : WB1;  // per-wave buffer
+  static constexpr int WB = WB0 > CPW * PC ? WB0 : CPW * PC;  // per-wave buffer
   static constexpr int DY = TY * P + 1, DZ = TZ * P + 1, PL = DY * DZ;
   static constexpr int DZP = DZ | 1, PLP = DY * DZP;
 };
 
-// MFMA 16x16x4 in both precisions (cdna_hip_programming.md §3): A[m][k] at
-// lane m + 16k, B[k][n] at lane n + 16k (one value per lane); D[m][n] at
-// lane n + 16 g, register r with m = 4g + r (f32) or m = g + 4r (f64).
-template <typename T> struct F5Mfma;
-template <> struct F5Mfma<float> {
-  typedef float V4 __attribute__((ext_vector_type(4)));
-  static __device__ __forceinline__ V4 mma(float a, float b, V4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  static __host__ __device__ constexpr int row(int g, int r) { return 4 * g + r; }
-};
-template <> struct F5Mfma<double> {
-  typedef double V4 __attribute__((ext_vector_type(4)));
-  static __device__ __forceinline__ V4 mma(double a, double b, V4 c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-  }
-  static __host__ __device__ constexpr int row(int g, int r) { return g + 4 * r; }
-};
-
 // fused5: nodal x / z / y Kronecker passes for parallelepiped cells, P = 3..7.
-// MF = 1 (axis-aligned cells, ND >= 6): the three passes as MFMA GEMMs with
-// the stacked 1D matrices as constant A operands (no scalar table loads):
-//   x: [K; M] (16 x 8) . u[l][(j, k)]                -> Kx u, Mx u
-//   z: [M; K] . (Kx u)[k][(i, j)], [K; M] . (Mx u)    -> zM = G00 Mz Kx u + G22 Kz Mx u,
-//                                                        zK = G11 Mz Mx u (same lanes)
-//   y: [My | Ky] (16 x 16) . [zM; zK][(j', arr)][(i, k)] -> y_e
-template <typename T, int ND, int NARR, int MODE, int MF = 0>
-__global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
+// (An MFMA form of the three passes lost to this VALU core at Q6 in both
+// precisions: profiles/r2_fused5_mfma.md, profiles/r3_mfma.md.)
+template <typename T, int ND, int NARR, int MODE>
+__global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
     lap_fused5_kernel(Fused2Args<T> A, const T* __restrict__ tabd) {
-  using S = F5Shape<T, ND, NARR, MF>;
-  static_assert(!MF || (NARR == 2 && S::CPW == 1 && ND <= 8), "MFMA core: 2-array, one cell per wave");
+  using S = F5Shape<T, ND, NARR>;
   constexpr int P = S::P, CPW = S::CPW, TY = S::TY, TZ = S::TZ;
   constexpr int DY = S::DY, DZ = S::DZ, PL = S::PL, DZP = S::DZP, PLP = S::PLP;
   constexpr int NT = S::NT, ND2 = ND * ND, NDP = S::NDP, ARR = S::ARR, WB = S::WB;
@@ -247,8 +166,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
   const int la = ab / ND, lb = ab % ND;
   const int c = wv * CPW + cw;
   const int cy = c / TZ, cz = c % TZ;
-  // MF: every lane of the wave works on its cell (the MFMA lane maps use all 64)
-  const bool cell_on = (MF || lane_on) && (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
+  const bool cell_on = lane_on && (ty * TY + cy < A.n1) && (tz * TZ + cz < A.n2);
   T* const Wb = s_w + wv * WB;             // this wave's buffer
   T* const Wc = Wb + cw * ND2 * NDP;       // this cell's rows of array 0
 
@@ -424,129 +342,55 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
   // x-march (4 ND^2 doubles would not fit the SGPR file).
   typedef const __attribute__((address_space(4))) T CT;
   CT* const tab0 = (CT*)tabd;
-  // BDX_F5_LBASE: launder one base pointer per row and address the row by a
+  // One base pointer is laundered per row and the row is addressed by a
   // constant offset (folded into the scalar load's immediate) -- otherwise
   // the compiler hoists every row pointer out of the x-march and the ~40
-  // SGPR pairs spill to VGPR lanes (v_readlane per use in the loop)
+  // SGPR pairs spill to VGPR lanes (v_readlane per use in the loop).
   CT* tabl = tab0;
   // out[a] (+)= s * sum_b Mat[a][b] in[b]; id 0 = M, 1 = K, 2 = C, 3 = C^T.
-  // Row a's pointer is laundered through an asm that consumes the result of
-  // row a - 2 (d2): the scalar loads run one row ahead of the FMAs and at
-  // most two rows are live in SGPRs.
-  // MFMA A operands (lane m + 16k holds A[m][k]): [K; M], [M; K] over k-steps
-  // of 4, and [My | Ky] (16 x 16) over 4 k-steps
-  T aKM[2] = {T(0), T(0)}, aMK[2] = {T(0), T(0)}, aY[4] = {T(0), T(0), T(0), T(0)};
-  if constexpr (MF) {
-    const int am = lane & 15, ak = lane >> 4;
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const int l = 4 * st + ak, rr = am & 7;
-      const T k_ = tabd[64 + rr * kF5Stride + l], m_ = tabd[rr * kF5Stride + l];
-      aKM[st] = am < 8 ? k_ : m_;
-      aMK[st] = am < 8 ? m_ : k_;
-    }
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int kap = 4 * st + ak, id = kap >> 3, c_ = kap & 7;
-      aY[st] = am < 8 ? tabd[id * 64 + am * kF5Stride + c_] : T(0);
-    }
-  }
+  // The base is laundered through an asm that consumes the result of row
+  // a - 2 (d2): the scalar loads run one row ahead of the FMAs and at most
+  // two rows are live in SGPRs.
   T d1 = T(0), d2 = T(0);
-  constexpr int EOM = BDX_F5_EO ? (sizeof(T) == 4 ? BDX_F5_EO_F32 : BDX_F5_EO_F64) : 0;
-  auto matvec = [&](int id, const T (&in)[ND], T (&out)[ND], T s, bool acc, int pass) {
-    if constexpr (EOM != 0 && BDX_F5_PK && sizeof(T) == 4) {
-      if (id < 2 && (EOM & pass)) {
-        // FP32 even-odd with packed math: (even, odd) sums of a line pair in
-        // one v_pk_add_f32, (E, O) row products in v_pk_fma_f32 against the
-        // interleaved table rows (one SGPR pair per product)
-        typedef float F2 __attribute__((ext_vector_type(2)));
-        typedef const __attribute__((address_space(4))) F2 CF2;
-        constexpr int H = ND / 2, ODD = ND % 2;
-        F2 eo[H];
+  auto matvec = [&](int id, const T (&in)[ND], T (&out)[ND], T s, bool acc) {
+    if (id < 2) {  // M or K: even-odd form (compile-time after inlining)
+      constexpr int H = ND / 2, ODD = ND % 2;
+      T ev[H], od[H];
 #pragma unroll
-        for (int b = 0; b < H; ++b) eo[b] = F2{in[b], in[b]} + F2{in[ND - 1 - b], -in[ND - 1 - b]};
-#pragma unroll
-        for (int a = 0; a < H + ODD; ++a) {
-          asm volatile("" : "+s"(tabl) : "v"(d2));
-          CF2* rp = reinterpret_cast<CF2*>(tabl + kF5PK + id * 32 + a * 8);
-          F2 t2 = rp[0] * eo[0];
-#pragma unroll
-          for (int b = 1; b < H; ++b) t2 = rp[b] * eo[b] + t2;
-          T te = t2.x;
-          if constexpr (ODD) te += rp[H].x * in[H];
-          if (a < H) {
-            const T r1 = te + t2.y, r2 = te - t2.y;
-            out[a] = acc ? out[a] + s * r1 : s * r1;
-            out[ND - 1 - a] = acc ? out[ND - 1 - a] + s * r2 : s * r2;
-            d2 = d1;
-            d1 = r1;
-          } else {
-            out[a] = acc ? out[a] + s * te : s * te;
-            d2 = d1;
-            d1 = te;
-          }
-        }
-        return;
+      for (int b = 0; b < H; ++b) {
+        ev[b] = in[b] + in[ND - 1 - b];
+        od[b] = in[b] - in[ND - 1 - b];
       }
-    }
-    if constexpr (EOM != 0) {
-      if (id < 2 && (EOM & pass)) {  // M or K: even-odd form (compile-time after inlining)
-        constexpr int H = ND / 2, ODD = ND % 2;
-        T ev[H], od[H];
 #pragma unroll
-        for (int b = 0; b < H; ++b) {
-          ev[b] = in[b] + in[ND - 1 - b];
-          od[b] = in[b] - in[ND - 1 - b];
+      for (int a = 0; a < H + ODD; ++a) {
+        asm volatile("" : "+s"(tabl) : "v"(d2));
+        CT* re = tabl + kF5EO + id * 32 + a * 4;
+        T te = T(0);
+#pragma unroll
+        for (int b = 0; b < H; ++b) te += re[b] * ev[b];
+        if constexpr (ODD) te += re[H] * in[H];
+        if (a < H) {
+          CT* ro = tabl + kF5EO + id * 32 + 16 + a * 4;
+          T to = T(0);
+#pragma unroll
+          for (int b = 0; b < H; ++b) to += ro[b] * od[b];
+          const T r1 = te + to, r2 = te - to;
+          out[a] = acc ? out[a] + s * r1 : s * r1;
+          out[ND - 1 - a] = acc ? out[ND - 1 - a] + s * r2 : s * r2;
+          d2 = d1;
+          d1 = r1;
+        } else {
+          out[a] = acc ? out[a] + s * te : s * te;
+          d2 = d1;
+          d1 = te;
         }
-#pragma unroll
-        for (int a = 0; a < H + ODD; ++a) {
-          CT* re;
-          if (BDX_F5_LBASE) {
-            asm volatile("" : "+s"(tabl) : "v"(d2));
-            re = tabl + kF5EO + id * 32 + a * 4;
-          } else {
-            re = tab0 + kF5EO + id * 32 + a * 4;
-            asm volatile("" : "+s"(re) : "v"(d2));
-          }
-          T te = T(0);
-#pragma unroll
-          for (int b = 0; b < H; ++b) te += re[b] * ev[b];
-          if constexpr (ODD) te += re[H] * in[H];
-          if (a < H) {
-            CT* ro;
-            if (BDX_F5_LBASE) {
-              ro = tabl + kF5EO + id * 32 + 16 + a * 4;
-            } else {
-              ro = tab0 + kF5EO + id * 32 + 16 + a * 4;
-              asm volatile("" : "+s"(ro) : "v"(d2));
-            }
-            T to = T(0);
-#pragma unroll
-            for (int b = 0; b < H; ++b) to += ro[b] * od[b];
-            const T r1 = te + to, r2 = te - to;
-            out[a] = acc ? out[a] + s * r1 : s * r1;
-            out[ND - 1 - a] = acc ? out[ND - 1 - a] + s * r2 : s * r2;
-            d2 = d1;
-            d1 = r1;
-          } else {
-            out[a] = acc ? out[a] + s * te : s * te;
-            d2 = d1;
-            d1 = te;
-          }
-        }
-        return;
       }
+      return;
     }
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
-      CT* row;
-      if (BDX_F5_LBASE) {
-        asm volatile("" : "+s"(tabl) : "v"(d2));
-        row = tabl + id * 64 + a * kF5Stride;
-      } else {
-        row = tab0 + id * 64 + a * kF5Stride;
-        asm volatile("" : "+s"(row) : "v"(d2));
-      }
+      asm volatile("" : "+s"(tabl) : "v"(d2));
+      CT* row = tabl + id * 64 + a * kF5Stride;
       T t = T(0);
 #pragma unroll
       for (int b = 0; b < ND; ++b) t += row[b] * in[b];
@@ -582,7 +426,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
-      if (!(BDX_F5_DROP & 4) && !last && (st_meta[k] & kValid)) {
+      if (!last && (st_meta[k] & kValid)) {
         if (BDX_OOB(lnext + st_goff[k], A.vsize, "f5 prefetch")) continue;
         pf_r[k] = ld_stream(un_r + st_goff[k]);
         if constexpr (MODE == kFusedCG) {
@@ -635,105 +479,6 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     (void)G12;
 
     const T* __restrict__ ucell = su + (cy * P) * DZP + cz * P;
-    if constexpr (MF) {
-      using MM = F5Mfma<T>;
-      using V4 = typename MM::V4;
-      constexpr int ND2 = ND * ND, ND3 = ND2 * ND;
-      constexpr int ZT = sizeof(T) == 8 ? 2 : 4;  // z-pass tiles per group
-      const int n16 = lane & 15, g4 = lane >> 4;
-      T* const Wx = Wb;             // Kx u, Mx u: [arr][i][j][k]
-      T* const Wz = Wb + 2 * ND3;   // zM, zK:     [arr][i][j][k]
-      // ---- x pass: D[(arr, i)][(j, k)] = [K; M][(arr, i)][l] u[l][(j, k)]
-      V4 ax[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) ax[t] = V4{0, 0, 0, 0};
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int l = 4 * st + g4;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int n = 16 * t + n16;
-          const bool ok = n < ND2 && l < ND;
-          const T b = ok ? ucell[l * PLP + (n / ND) * DZP + n % ND] : T(0);
-          ax[t] = MM::mma(aKM[st], b, ax[t]);
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int n = 16 * t + n16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = MM::row(g4, r);
-          if (n < ND2 && (m & 7) < ND) Wx[(m >> 3) * ND3 + (m & 7) * ND2 + n] = ax[t][r];
-        }
-      }
-      wave_sync();
-      // ---- z pass: columns (i, j), contraction over k; two tiles at a time
-      // (4 accumulators live: the FP64 instance otherwise spills)
-#pragma unroll
-      for (int h = 0; h < 4; h += ZT) {
-        V4 z1[ZT], z2[ZT];
-#pragma unroll
-        for (int t = 0; t < ZT; ++t) z1[t] = z2[t] = V4{0, 0, 0, 0};
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const int k = 4 * st + g4;
-#pragma unroll
-          for (int t = 0; t < ZT; ++t) {
-            const int n = 16 * (h + t) + n16;
-            const bool ok = n < ND2 && k < ND;
-            const T b1 = ok ? Wx[n * ND + k] : T(0);
-            const T b2 = ok ? Wx[ND3 + n * ND + k] : T(0);
-            z1[t] = MM::mma(aMK[st], b1, z1[t]);
-            z2[t] = MM::mma(aKM[st], b2, z2[t]);
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < ZT; ++t) {
-          const int n = 16 * (h + t) + n16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = MM::row(g4, r);
-            const T v = m < 8 ? G00 * z1[t][r] + G22 * z2[t][r] : G11 * z2[t][r];
-            if (n < ND2 && (m & 7) < ND) Wz[(m >> 3) * ND3 + n * ND + (m & 7)] = v;
-          }
-        }
-      }
-      wave_sync();
-      // ---- y pass: columns (i, k), contraction over (arr, j')
-      V4 ya[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) ya[t] = V4{0, 0, 0, 0};
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int kap = 4 * st + g4, arr = kap >> 3, jp = kap & 7;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int n = 16 * t + n16;
-          const bool ok = n < ND2 && jp < ND;
-          const T b = ok ? Wz[arr * ND3 + (n / ND) * ND2 + jp * ND + n % ND] : T(0);
-          ya[t] = MM::mma(aY[st], b, ya[t]);
-        }
-      }
-      // element dot and element vector E[j][k][i] (Wx is dead: E overlays it)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int n = 16 * t + n16;
-        const int i = n / ND, kq = n % ND;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = MM::row(g4, r);
-          if (n < ND2 && j < ND) {
-            const T ye = ya[t][r];
-            if constexpr (MODE == kFusedCG) {
-              if (cell_on && !red)
-                pap += static_cast<double>(ucell[i * PLP + j * DZP + kq]) * static_cast<double>(ye);
-            }
-            Wb[j * ND2 + kq * ND + i] = cell_on ? ye : T(0);
-          }
-        }
-      }
-    } else {
     // ------------------------------------------------ x pass: lane (j, k) = (la, lb)
     {
       T u[ND];
@@ -748,21 +493,21 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
           for (int i = 0; i < ND; ++i) w[i * ND * NDP] = o[i];
         }
       };
-      matvec(1, u, o, T(1), false, 1);
+      matvec(1, u, o, T(1), false);
       put(0);
-      matvec(0, u, o, T(1), false, 1);
+      matvec(0, u, o, T(1), false);
       put(1);
       if constexpr (MIXED) {
-        matvec(2, u, o, T(1), false, 1);
+        matvec(2, u, o, T(1), false);
         put(2);
-        matvec(3, u, o, T(1), false, 1);
+        matvec(3, u, o, T(1), false);
         put(3);
       }
     }
     wave_sync();
 
     // ------------------------------------------------ z pass: lane (i, j) = (la, lb)
-    if constexpr ((BDX_F5_DROP & 1) == 0 && !MIXED && BDX_F5_ZSPLIT) {
+    if constexpr (!MIXED) {
       // both input rows of every lane are in registers once the loads have
       // returned (one ds_read per row for the whole wave), so zK can be
       // written back before zM is formed: one output row live, not two
@@ -773,7 +518,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       T* w = Wc + la * ND * NDP + lb;
       {
         T zK[ND];
-        matvec(0, am, zK, G11, false, 2);
+        matvec(0, am, zK, G11, false);
         wave_sync();
         if (lane_on) {
 #pragma unroll
@@ -781,33 +526,33 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
         }
       }
       T zM[ND];
-      matvec(0, ak, zM, G00, false, 2);
-      matvec(1, am, zM, G22, true, 2);
+      matvec(0, ak, zM, G00, false);
+      matvec(1, am, zM, G22, true);
       if (lane_on) {
 #pragma unroll
         for (int k = 0; k < ND; ++k) w[k * NDP] = zM[k];
       }
       wave_sync();
-    } else if constexpr ((BDX_F5_DROP & 1) == 0) {
+    } else {
       const T* r = Wc + ab * NDP;
       T ak[ND], am[ND];
       ldrow<ND>(r, ak);
       ldrow<ND>(r + ARR, am);
       T zM[ND], zK[ND];
-      matvec(0, ak, zM, G00, false, 2);
-      matvec(1, am, zM, G22, true, 2);
-      matvec(0, am, zK, G11, false, 2);
+      matvec(0, ak, zM, G00, false);
+      matvec(1, am, zM, G22, true);
+      matvec(0, am, zK, G11, false);
       if constexpr (MIXED) {
         T ac[ND], at[ND];
         ldrow<ND>(r + 2 * ARR, ac);
         ldrow<ND>(r + 3 * ARR, at);
         T zCt[ND], zC[ND];
-        matvec(3, ac, zM, G02, true, 2);
-        matvec(2, at, zM, G02, true, 2);
-        matvec(0, ac, zCt, G01, false, 2);
-        matvec(2, am, zCt, G12, true, 2);
-        matvec(0, at, zC, G01, false, 2);
-        matvec(3, am, zC, G12, true, 2);
+        matvec(3, ac, zM, G02, true);
+        matvec(2, at, zM, G02, true);
+        matvec(0, ac, zCt, G01, false);
+        matvec(2, am, zCt, G12, true);
+        matvec(0, at, zC, G01, false);
+        matvec(3, am, zC, G12, true);
         wave_sync();
         // rows [i][k][j]: lane (i, j) writes column j of rows (i, k)
         if (lane_on) {
@@ -839,14 +584,14 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
       T sM[ND], sK[ND];
       ldrow<ND>(r, sM);
       ldrow<ND>(r + ARR, sK);
-      matvec(0, sM, ye, T(1), false, 4);
-      matvec(1, sK, ye, T(1), true, 4);
+      matvec(0, sM, ye, T(1), false);
+      matvec(1, sK, ye, T(1), true);
       if constexpr (MIXED) {
         T sCt[ND], sC[ND];
         ldrow<ND>(r + 2 * ARR, sCt);
         ldrow<ND>(r + 3 * ARR, sC);
-        matvec(3, sCt, ye, T(1), true, 4);
-        matvec(2, sC, ye, T(1), true, 4);
+        matvec(3, sCt, ye, T(1), true);
+        matvec(2, sC, ye, T(1), true);
       }
     }
     // element dot p_e . (A_e p_e): lane holds y_e[i = la][j][k = lb]
@@ -863,17 +608,14 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
 #pragma unroll
       for (int j = 0; j < ND; ++j) eo[j * P1] = cell_on ? ye[j] : T(0);
     }
-    }
     __syncthreads();
 
     auto do_gather = [&]() __attribute__((always_inline)) {
       // ------------------------------------------------ gather-sum and write out
-      if constexpr ((BDX_F5_DROP & 2) == 0) {
-        if (BDX_F5_LAUNDER & 1) {
+      {
   #pragma unroll
-          for (int k = 0; k < NOUT; ++k)
-            asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
-        }
+        for (int k = 0; k < NOUT; ++k)  // descriptor laundering (see the file head)
+          asm volatile("" : "+v"(o_src[k][0]), "+v"(o_src[k][1]), "+v"(o_off[k]), "+v"(o_meta[k]));
         const int64_t lbase = static_cast<int64_t>(cx) * P;
         T* __restrict__ ybase[4] = {A.y + lbase * A.ps, A.yb + lbase * A.ybps,
                                     A.zb + lbase * A.zbps, A.cb + lbase * A.cbps};
@@ -915,10 +657,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
     auto do_stage = [&]() __attribute__((always_inline)) {
       // ------------------------------------------------ stage the next layer
       if (!last) {
-        if (BDX_F5_LAUNDER & 2) {
   #pragma unroll
-          for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
-        }
+        for (int k = 0; k < NPF; ++k) asm volatile("" : "+v"(st_goff[k]), "+v"(st_meta[k]));
         T* __restrict__ un = s_u[nxt];
   #pragma unroll
         for (int k = 0; k < NCP; ++k)
@@ -974,20 +714,15 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR, MF>::NT), BDX_F5_WAVES)
         }
       }
     };
-    // BDX_F5_STAGE_FIRST: consume the prefetch (wait for the loads) before
-    // the gather issues its stores, so the wait does not drain them
-    if constexpr (BDX_F5_STAGE_FIRST) {
-      // one explicit, unconditional vmcnt(0) (gfx9 encoding; expcnt and
-      // lgkmcnt untouched): the prefetch has landed and no store of this
-      // layer is pending yet, so the waitcnt pass sees nothing outstanding
-      // and does not put a draining wait before each slot's stores
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      do_stage();
-      do_gather();
-    } else {
-      do_gather();
-      do_stage();
-    }
+    // Consume the prefetch (wait for the loads) before the gather issues its
+    // stores, so the wait does not drain them: one explicit, unconditional
+    // vmcnt(0) (gfx9 encoding; expcnt and lgkmcnt untouched).  The prefetch
+    // has landed and no store of this layer is pending yet, so the waitcnt
+    // pass sees nothing outstanding and does not put a draining wait before
+    // each slot's stores.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    do_stage();
+    do_gather();
     kc_cur = kc_nxt;
   }
   if constexpr (MODE == kFusedCG) {
@@ -1044,45 +779,16 @@ inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, co
       }
       if (odd) E[a * 4 + h] = static_cast<T>(Mx[a][h]);
     }
-    T* PK = out + kF5PK + id * 32;
-    for (int a = 0; a < h + odd; ++a) {
-      for (int b = 0; b < h; ++b) {
-        PK[a * 8 + 2 * b] = E[a * 4 + b];
-        PK[a * 8 + 2 * b + 1] = a < h ? O[a * 4 + b] : T(0);
-      }
-      if (odd) PK[a * 8 + 2 * h] = E[a * 4 + h];
-    }
   }
   return kFusedTabMax;
 }
 
 // affine_ok: 0 = general cells (refused), 1 = parallelepipeds, 2 = axis-aligned
 // boxes (diagonal Jacobians: the 2-array instance)
-// MFMA core for the axis-aligned instances with one cell per wave (ND >= 6):
-// BDX_F5_MFMA=1|0 at launch time (A/B and tests; a captured graph keeps the
-// instance it was captured with).  Default off: same-box A/B at Q6 500 M,
-// MFMA vs VALU core, FP32 55.2 vs 59.9 GDoF/s, FP64 33.8 vs 45.9 (the FP64
-// instance spills 28 dwords); PMC: scalar loads 3.4e8 -> 4e5, LDS
-// instructions 1.7e8 -> 3.0e8 (element-granular operand staging), waits
-// +60 % (profiles/r2_fused5_mfma.md).
-#ifndef BDX_F5_MFMA_DEFAULT
-#define BDX_F5_MFMA_DEFAULT 0
-#endif
-inline bool fused5_mfma() {
-  const char* e = std::getenv("BDX_F5_MFMA");
-  return e ? std::atoi(e) != 0 : BDX_F5_MFMA_DEFAULT != 0;
-}
-
 template <typename T, int ND, int MODE>
 int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStream_t st) {
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
-  if constexpr (ND >= 6) {
-    if (affine_ok == 2 && fused5_mfma()) {
-      lap_fused5_kernel<T, ND, 2, MODE, 1><<<nblk, F5Shape<T, ND, 2, 1>::NT, 0, st>>>(a, tabd);
-      return static_cast<int>(hipGetLastError());
-    }
-  }
   if (affine_ok == 2)
     lap_fused5_kernel<T, ND, 2, MODE><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
   else
@@ -1132,7 +838,6 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
                                                   T* out) {                        \
     return pack_tables5<T>(nd, nq, phi0, Dd, wts, out);                            \
   }                                                                                \
-  extern "C" int bdx_drop_flags_f5_##SUF##_p##PP() { return BDX_F5_DROP; }          \
   extern "C" int bdx_fused5_segments_##SUF##_p##PP(int affine_ok, int tiles, int ncx) { \
     int per_cu = 0, dev = 0, cus = 0;                                              \
     hipError_t e = hipGetDevice(&dev);                                             \
@@ -1149,7 +854,8 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     return e == hipSuccess ? fused_choose_segments(tiles, ncx, per_cu * cus) : 1;  \
   }                                                                                \
   extern "C" int bdx_fused5_tile_p##PP##_##SUF(int affine_ok, int* ty, int* tz) {  \
-    *ty = affine_ok == 2 ? F5Tile<PP + 1, 2>::TY : F5Tile<PP + 1, 4>::TY;          \
-    *tz = affine_ok == 2 ? F5Tile<PP + 1, 2>::TZ : F5Tile<PP + 1, 4>::TZ;          \
+    (void)affine_ok;                                                               \
+    *ty = F5Tile<PP + 1>::TY;                                                      \
+    *tz = F5Tile<PP + 1>::TZ;                                                      \
     return 0;                                                                      \
   }

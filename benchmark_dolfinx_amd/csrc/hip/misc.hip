@@ -115,6 +115,10 @@ BDX_MISC_API(double, f64)
 BDX_MISC_API(float, f32)
 
 // Device banner (reference get_device_information, src/util.cpp:10-52).
+// 1 when the library was built with the device bounds checks (BDX_DEBUG):
+// correct numerics, but not a valid timing build.
+int bdx_build_debug() { return BDX_DEBUG; }
+
 int bdx_device_info(int dev, char* buf, int buflen) {
   hipDeviceProp_t p;
   hipError_t e = hipGetDeviceProperties(&p, dev);

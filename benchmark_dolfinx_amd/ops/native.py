@@ -101,29 +101,17 @@ def hip():
 
 def build_flags() -> dict:
     """Build facts of the loaded HIP library that decide whether a timing is
-    valid: the arch, the library file, and every timing-only phase-drop
-    macro compiled into it (BDX_UPD_DROP, BDX_F4_DROP, BDX_F5_DROP; nonzero
-    values skip work and give wrong numerics -- bench.py refuses them)."""
+    valid: the arch, the library file, and whether it is the production build
+    (the in-tree libbdx_hip.so, built with no extra flags) rather than an
+    A/B variant (BDX_HIP_LIB) or a bounds-checked debug build (BDX_DEBUG)."""
     lib = hip()
-    drops = {}
-    for name, key in (("bdx_drop_flags_common", "BDX_UPD_DROP"),
-                      ("bdx_drop_flags_f4", "BDX_F4_DROP"),
-                      ("bdx_drop_flags_f23", "BDX_X_*/BDX_X3_*")):
-        if hasattr(lib, name):
-            fn = getattr(lib, name)
-            fn.restype = ctypes.c_int
-            drops[key] = int(fn())
-    f5 = 0
-    for suf in ("f64", "f32"):
-        for P in range(1, 8):
-            name = f"bdx_drop_flags_f5_{suf}_p{P}"
-            if hasattr(lib, name):
-                fn = getattr(lib, name)
-                fn.restype = ctypes.c_int
-                f5 |= int(fn())
-    drops["BDX_F5_DROP"] = f5
-    return {"arch": _build.HIP_ARCH, "hiplib": os.path.basename(_loaded.get("hip", "")),
-            "drops": drops, "valid": not any(drops.values())}
+    fn = lib.bdx_build_debug
+    fn.restype = ctypes.c_int
+    debug = int(fn())
+    path = _loaded.get("hip", "")
+    production = os.path.abspath(path) == os.path.abspath(str(_build.HIP_SO))
+    return {"arch": _build.HIP_ARCH, "hiplib": os.path.basename(path), "debug": debug,
+            "production": production, "valid": production and not debug}
 
 
 def loaded_libraries() -> list[str]:

@@ -285,18 +285,6 @@ def test_fused5_action_and_cg(nc, P, qm, g, shear, dt, coef):
     op.close()
 
 
-@pytest.mark.parametrize("coef", ["constant", "random"])
-@pytest.mark.parametrize("nc,P,dt", [((2, 3, 3), 5, torch.float64), ((2, 2, 3), 6, torch.float64),
-                                     ((3, 2, 2), 7, torch.float64), ((2, 3, 2), 6, torch.float32),
-                                     ((2, 2, 2), 7, torch.float32)])
-def test_fused5_mfma_core(monkeypatch, nc, P, dt, coef):
-    """The MFMA instance of fused5 (BDX_F5_MFMA=1: v_mfma_f32/f64_16x16x4 with
-    the stacked 1D matrices as A operands, one cell per wave) against the C++
-    CPU operator, and its CG against the host CG."""
-    monkeypatch.setenv("BDX_F5_MFMA", "1")
-    test_fused5_action_and_cg(nc, P, 1, False, 0.0, dt, coef)
-
-
 def _cg_job_f5(comm, nc, P, nreps, shear):
     pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", 0.0, "random", shear)
     u = pb.assemble_rhs()
