@@ -72,20 +72,23 @@ int launch_geometry(int nq, const BdxLattice& lat, const OpTables<T>& tb,
   return static_cast<int>(hipGetLastError());
 }
 
-// Wave-per-row CSR SpMV (the reference's assembled-matrix comparison operator).
+// Wave-per-row CSR SpMV (the reference's assembled-matrix comparison
+// operator) over the entry range [beg[row], end[row]) of each row; acc = 1
+// adds to y.  Two launches with a column-split matrix give the reference's
+// owned-column / ghost-column overlap (src/csr.hpp:203-217).
 template <typename T>
 __global__ void __launch_bounds__(256)
-    spmv_kernel(int64_t nrows, const int64_t* __restrict__ row_ptr,
+    spmv_kernel(int64_t nrows, const int64_t* __restrict__ beg, const int64_t* __restrict__ end,
                 const int32_t* __restrict__ cols, const T* __restrict__ vals,
-                const T* __restrict__ x, T* __restrict__ y) {
+                const T* __restrict__ x, T* __restrict__ y, int acc_out) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= nrows) return;
-  const int64_t b = row_ptr[row], e = row_ptr[row + 1];
+  const int64_t b = beg[row], e = end[row];
   T acc = 0;
   for (int64_t p = b + lane; p < e; p += 64) acc += vals[p] * x[cols[p]];
   acc = wave_sum(acc);
-  if (lane == 0) y[row] = acc;
+  if (lane == 0) y[row] = acc_out ? y[row] + acc : acc;
 }
 
 }  // namespace
@@ -102,12 +105,12 @@ extern "C" {
                                              phi0, dphi1, wts, qpts, 0);      \
     return launch_geometry<T>(nq, lat, tb, xv, G, st);                        \
   }                                                                           \
-  int bdx_spmv_##SUF(int64_t nrows, const int64_t* row_ptr,                   \
+  int bdx_spmv_##SUF(int64_t nrows, const int64_t* beg, const int64_t* end,    \
                      const int32_t* cols, const T* vals, const T* x, T* y,    \
-                     hipStream_t st) {                                        \
+                     int acc, hipStream_t st) {                               \
     if (nrows <= 0) return 0;                                                 \
     spmv_kernel<T><<<static_cast<unsigned>((nrows + 3) / 4), 256, 0, st>>>(   \
-        nrows, row_ptr, cols, vals, x, y);                                    \
+        nrows, beg, end, cols, vals, x, y, acc);                              \
     return static_cast<int>(hipGetLastError());                               \
   }
 

@@ -516,15 +516,14 @@ int bdx_host_version() { return 1; }
     return csr_build<T>(latd, nq, B, Dd, wts, qpts, xv, kappa, kc, row_ptr,   \
                         cols, vals, count_only);                              \
   }                                                                           \
-  void bdx_cpu_spmv_##SUF(int64_t nrows, const int64_t* row_ptr,              \
+  void bdx_cpu_spmv_##SUF(int64_t nrows, const int64_t* beg, const int64_t* end, \
                           const int32_t* cols, const T* vals, const T* x,     \
-                          T* y) {                                             \
+                          T* y, int acc) {                                    \
     _Pragma("omp parallel for schedule(static)") for (int64_t r = 0;          \
                                                       r < nrows; ++r) {       \
       T s = 0;                                                                \
-      for (int64_t p = row_ptr[r]; p < row_ptr[r + 1]; ++p)                   \
-        s += vals[p] * x[cols[p]];                                            \
-      y[r] = s;                                                               \
+      for (int64_t p = beg[r]; p < end[r]; ++p) s += vals[p] * x[cols[p]];    \
+      y[r] = acc ? y[r] + s : s;                                              \
     }                                                                         \
   }                                                                           \
   /* f = 1000 exp(-((x-1/2)^2 + (y-1/2)^2)/0.02) at the physical dof nodes */ \

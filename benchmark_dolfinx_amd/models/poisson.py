@@ -340,24 +340,48 @@ class CSROperator:
             fn(*args, ptr(row_ptr), ptr(cols), ptr(vals), 0)
         self.nnz = int(nnz)
         self.nrows = lat.nstore
+        # Column split of every row, as DOLFINx's MatrixCSR off-diagonal block
+        # (src/csr.hpp:203-217): entries [row_ptr, off) read columns this rank
+        # owns or computes itself, [off, row_ptr + 1) the ghost columns that the
+        # forward halo exchange fills -- so the first pass overlaps it.
+        ghost = np.zeros(lat.nstore, dtype=bool)
+        halo = problem.halo
+        if getattr(halo, "active", False):
+            ghost[halo.ghosts.index.cpu().numpy()] = True
+        rows = np.repeat(np.arange(lat.nstore, dtype=np.int64), np.diff(row_ptr))
+        g = ghost[cols]
+        order = np.lexsort((g, rows))  # stable: by row, owned columns first
+        cols, vals = np.ascontiguousarray(cols[order]), np.ascontiguousarray(vals[order])
+        off = row_ptr[:-1] + np.bincount(rows[~g], minlength=lat.nstore).astype(np.int64)
+        self.nghost_entries = int(g.sum())
         with timed("% Copy to GPU MatrixCSR" if problem.platform == "gpu"
                    else "% Copy CSR"):
-            self.row_ptr = torch.from_numpy(row_ptr).to(problem.device)
-            self.cols = torch.from_numpy(cols).to(problem.device)
-            self.vals = torch.from_numpy(vals).to(problem.device)
+            dev = problem.device
+            self.row_ptr = torch.from_numpy(row_ptr).to(dev)
+            self.off = torch.from_numpy(off).to(dev)
+            self.cols = torch.from_numpy(cols).to(dev)
+            self.vals = torch.from_numpy(vals).to(dev)
         self._host = (row_ptr, cols, vals)
 
     def frobenius_norm(self) -> float:
         s = float(torch.sum(self.vals.double() ** 2).item())
         return math.sqrt(self.pb.comm.allreduce_scalar(s))
 
-    def apply(self, x: torch.Tensor, y: torch.Tensor) -> None:
+    def _spmv(self, beg, end, x, y, acc):
         pb = self.pb
-        pb.halo.forward(x)
         if pb.platform == "gpu":
-            pb.kernels.spmv(self.nrows, self.row_ptr, self.cols, self.vals, x, y)
+            pb.kernels.spmv(self.nrows, beg, end, self.cols, self.vals, x, y, acc)
         else:
             getattr(native.host(), f"bdx_cpu_spmv_{pb.suf}")(
-                self.nrows, ptr(self.row_ptr.numpy()), ptr(self.cols.numpy()),
-                ptr(self.vals.numpy()), ptr(x.numpy()), ptr(y.numpy()))
+                self.nrows, ptr(beg.numpy()), ptr(end.numpy()), ptr(self.cols.numpy()),
+                ptr(self.vals.numpy()), ptr(x.numpy()), ptr(y.numpy()), int(acc))
+
+    def apply(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        """y = A x: owned-column pass while the forward exchange is in
+        flight, ghost-column pass after it, reverse exchange of ghost rows."""
+        pb = self.pb
+        work = pb.halo.forward_begin(x)
+        self._spmv(self.row_ptr[:-1], self.off, x, y, False)
+        pb.halo.forward_end(x, work)
+        self._spmv(self.off, self.row_ptr[1:], x, y, True)
         pb.halo.reverse(y)

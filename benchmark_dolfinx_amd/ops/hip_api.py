@@ -36,7 +36,7 @@ def declare(lib) -> None:
         _d(lib, f"bdx_dofmap_apply_{suf}",
            [i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, f64, vp, vp, vp, vp])
         _d(lib, f"bdx_dofmap_geometry_{suf}", [i32, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp])
-        _d(lib, f"bdx_spmv_{suf}", [i64, vp, vp, vp, vp, vp, vp])
+        _d(lib, f"bdx_spmv_{suf}", [i64, vp, vp, vp, vp, vp, vp, i32, vp])
         for P in range(1, 8):
             name = f"bdx_fused_apply_{suf}_p{P}"
             if hasattr(lib, name):

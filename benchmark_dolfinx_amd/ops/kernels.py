@@ -119,9 +119,10 @@ class HipKernels:
                                        len(side.boxes), side.total, ptr(buf), _stream()),
                "box_copy")
 
-    def spmv(self, nrows, row_ptr, cols, vals, x, y):
-        _check(self._f("bdx_spmv")(nrows, ptr(row_ptr), ptr(cols), ptr(vals), ptr(x),
-                                   ptr(y), _stream()), "spmv")
+    def spmv(self, nrows, beg, end, cols, vals, x, y, acc=False):
+        """y[r] (+)= sum of vals[p] x[cols[p]] over p in [beg[r], end[r])."""
+        _check(self._f("bdx_spmv")(nrows, ptr(beg), ptr(end), ptr(cols), ptr(vals), ptr(x),
+                                   ptr(y), int(acc), _stream()), "spmv")
 
 
 def device_info(dev: int = 0) -> str:

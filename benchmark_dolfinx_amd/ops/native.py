@@ -69,7 +69,7 @@ def host():
                          [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_csr_{suf}",
                          [vp, i32, vp, vp, vp, vp, vp, ft, vp, vp, vp, vp, i32], i64)
-                _declare(lib, f"bdx_cpu_spmv_{suf}", [i64, vp, vp, vp, vp, vp])
+                _declare(lib, f"bdx_cpu_spmv_{suf}", [i64, vp, vp, vp, vp, vp, vp, i32])
                 _declare(lib, f"bdx_cpu_interp_f_{suf}", [vp, vp, vp, vp])
             _host = lib
     return _host
