@@ -194,8 +194,18 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
         allp = comm.gather_objects(phases)
         rec["phases_ms"] = phases
         rec["phases_ms_max_over_ranks"] = {
-            k: (all(p[k] for p in allp) if isinstance(phases[k], bool)
-                else max(p[k] for p in allp)) for k in phases}
+            k: (None if phases[k] is None else all(p[k] for p in allp)
+                if isinstance(phases[k], bool) else max(p[k] for p in allp)) for k in phases}
+        if n > 1:
+            # per-rank timeline of the split schedule: when the comm-stream
+            # chain (forward exchange, boundary tiles, reverse send) ended vs
+            # the interior tiles, ms from the iteration start
+            rec["phases_per_rank"] = [
+                {"comm_chain_done": round(p["t_halo_rev_done"], 4),
+                 "boundary_done": round(p["t_boundary_done"], 4),
+                 "interior_done": round(p["t_op_interior_done"], 4),
+                 "iteration": round(p["iteration"], 4),
+                 "hidden": p["halo_rev_hidden"]} for p in allp]
     log(f"{config}: {value:.2f} GDoF/s ({rec['ms_per_step']:.3f} ms/step, median "
         f"{med if med is None else round(med, 3)} ms; {rec['kernel']}, {rec['geometry']})")
     if hasattr(op, "close"):
@@ -322,6 +332,7 @@ def run(comm, a) -> dict | None:
             "comm": head["comm"],
             "phases_ms": head.get("phases_ms"),
             "phases_ms_max_over_ranks": head.get("phases_ms_max_over_ranks"),
+            "phases_per_rank": head.get("phases_per_rank"),
         },
         "q6_gdofs": companions.get("q6", {}).get("value"),
         "q6f32_gdofs": companions.get("q6f32", {}).get("value"),

@@ -3,7 +3,9 @@
 //
 // Inputs are the arrays a DOLFINx mesh carries (reference src/laplacian.hpp:
 // 105-114 and src/laplacian_gpu.hpp:153-170, built in src/mesh.cpp:87-102):
-//   cell_dofs  [ncells][ND^3]  cell -> dof map (tensor-product order i, j, k)
+//   cell_dofs  [ncells][ND^3]  cell -> dof map (tensor-product order i, j, k);
+//                              the sign bit marks the one (cell, local dof)
+//                              occurrence that writes a dof's CG vectors
 //   cell_verts [ncells][8]     cell -> geometry-node map (v = 4a + 2b + c)
 //   coords     [nverts][3]     geometry nodes
 //   dof_flags  [ndofs]         bit 0: Dirichlet dof, bit 1: owned by this rank
@@ -12,61 +14,628 @@
 //                              interior cells as in src/laplacian.hpp:281-349)
 // and optionally stored G [ncells][6][nq^3] (the reference layout) and a
 // per-cell coefficient.  Any hexahedral mesh, any cell order and any dof
-// numbering work: nothing is derived from a lattice.  The per-cell core is
-// v1's (lap_v1.h: one thread per quadrature point, sum factorisation through
-// LDS); the element vectors are scattered with float atomics like the
-// reference's kernel.  This path measures what the dofmap indirection costs;
-// the structured kernels (lap_fused*.h) are the performance path.
+// numbering work: nothing is derived from a lattice.
+//
+// Kernel design (MI355X, one wave per CPW = 64 / NQ^2 cells, no workgroup
+// barriers): the reference runs one thread per quadrature point with every
+// 1D contraction read from LDS behind a __syncthreads (10 per cell,
+// src/laplacian_gpu.hpp:172-412).  Here a lane owns a whole 1D line of the
+// cell and contracts it in registers; LDS only transposes between the line
+// directions, inside the wave:
+//   nodal      lane (i, j):   z-line of the element vector (gather, scatter)
+//   mixed      lane (i, qz):  y-lines of the half-interpolated arrays
+//   quadrature lane (qy, qz): x-lines of U, grad U, G grad U (G loads are
+//                             contiguous across these lanes), with the y- and
+//                             z-derivatives formed by lanes (qx, qz) / (qx, qy)
+// The stored-G loads of a cell are issued before its first contraction, so
+// they are in flight under the interpolation and gradient stages.
+//
+// CG mode fuses the reference's BLAS-1 calls (src/cg.hpp:121-167) into the
+// gather: p = r + beta p_old is formed per gathered dof, the designated
+// writer of each dof stores p and the lagged x += alpha p_old, the element
+// dots p_e . (A_e p_e) give p.Ap, and the y scatter-add uses float atomics as
+// the reference does.  With the update pass (r -= alpha y, r.r, y = 0) one
+// CG iteration moves 11 vector streams instead of the generic 15.
 #pragma once
 #include "lap_v1.h"
 
-// dofmap: v1 core on an explicit cell->dof / cell->vertex map (any hex mesh).
-template <typename T, int ND, int NQ, int GEOM>
-__global__ void __launch_bounds__(V1Shape<NQ>::threads)
-    lap_dofmap_kernel(const int* __restrict__ cells, int ncl, const int* __restrict__ cdofs,
-                      const int* __restrict__ cverts, const T* __restrict__ coords,
-                      const unsigned char* __restrict__ flags, OpTables<T> tb,
-                      const T* __restrict__ G, T kappa, const T* __restrict__ kc,
-                      const T* __restrict__ u, T* __restrict__ y) {
-  constexpr int nq3 = NQ * NQ * NQ, ND3 = ND * ND * ND;
-  constexpr int CPB = V1Shape<NQ>::cpb;
-  __shared__ V1Smem<T, ND, NQ> sm;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < NQ * ND; i += blockDim.x) sm.phi0[i] = tb.phi0[i];
-  for (int i = tid; i < NQ * NQ; i += blockDim.x) sm.dphi[i] = tb.dphi1[i];
+enum { kDofAction = 0, kDofCG = 1 };
+typedef unsigned bdx_u32x2 __attribute__((ext_vector_type(2)));
 
-  const int cs = tid / nq3;
-  const int q = tid - cs * nq3;
-  const int qx = q / (NQ * NQ), qy = (q / NQ) % NQ, qz = q % NQ;
-  const bool active = cs < CPB;
-  const int64_t li = static_cast<int64_t>(blockIdx.x) * CPB + cs;
-  const bool valid = active && li < ncl;
-  const int64_t cell = valid ? cells[li] : 0;
-  const bool is_dof = valid && qx < ND && qy < ND && qz < ND;
-  int dof = -1;
-  unsigned f = 0;
-  if (is_dof) {
-    dof = cdofs[cell * ND3 + (qx * ND + qy) * ND + qz];
-    BDX_DASSERT(dof >= 0);
-    f = flags[dof];
+template <int NQ>
+struct DofShape {
+  static constexpr int NQ2 = NQ * NQ;
+  static constexpr int CPW = NQ2 <= 64 ? 64 / NQ2 : 1;  // cells per wave
+  static constexpr int LPL = (NQ2 + 63) / 64;           // lines per lane (NQ = 9: 2)
+  static constexpr int NQP = NQ | 1;                    // odd z pitch: conflict-free z-lines
+  static constexpr int BUF = NQ * NQ * NQP;             // one transpose buffer per cell
+  static constexpr int WAVES = 4;
+  static constexpr int NT = 64 * WAVES;
+  // stored G of the lane's x-lines held in registers from the start of the
+  // cell (in flight under the interpolation and gradient); larger rules load
+  // it where it is used
+  static constexpr bool GPREF = 6 * NQ * LPL <= 30;
+};
+
+template <typename T>
+struct DofArgs {
+  const int* cells;
+  int ncl;
+  int cells_per_block;
+  int64_t nvec;  // entries of every vector (range of the buffer descriptors)
+  const int* cdofs;
+  const int* cverts;
+  const T* coords;
+  const unsigned char* flags;
+  const T* G;
+  const T* tab;  // device [phi0 (nq x nd) | dphi1 (nq x nq) | qpts | wts]
+  T kappa;
+  const T* kc;
+  const T* u;      // action: input; CG: r
+  const T* pold;   // CG
+  T* pnew;         // CG
+  T* x;            // CG
+  T* y;
+  const double* scal;
+  int beta_num, beta_den, xa_num, xa_den;  // -1: beta = 0 / no x update
+  double* partials;                        // CG: p.Ap per block
+};
+
+// wave-local LDS exchange (the lanes of one wave run in lockstep)
+__device__ __forceinline__ void dof_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// dofmap: line-per-lane sum factorisation on an explicit cell->dof map (any hex mesh).
+template <typename T, int ND, int NQ, int GEOM, int MODE>
+__global__ void __launch_bounds__(DofShape<NQ>::NT)
+    lap_dofmap_kernel(DofArgs<T> A) {
+  using S = DofShape<NQ>;
+  constexpr int CPW = S::CPW, LPL = S::LPL, NQP = S::NQP, BUF = S::BUF, NQ2 = NQ * NQ;
+  constexpr int ND3 = ND * ND * ND, NQ3 = NQ * NQ * NQ;
+  constexpr bool IDENT = ND == NQ;  // qmode 0, GLL: phi0 = I (quirk Q5 guarantees it)
+  constexpr bool GPREF = GEOM == kGeomStored && S::GPREF;
+  static_assert(ND * ND <= 64, "nodal z-lines: one per lane");
+  __shared__ __attribute__((aligned(16))) T s_buf[S::WAVES][CPW][3][BUF];
+  __shared__ T s_X[S::WAVES][CPW][24];
+  __shared__ int s_ids[S::WAVES][2][64];  // per-wave ring of cell ids (two blocks)
+  __shared__ double s_red[16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int slot = CPW > 1 ? lane / NQ2 : 0;
+  const int sl = lane - slot * NQ2;  // lane within the cell's slot (CPW > 1: < NQ2)
+  const bool slot_on = slot < CPW;
+  T* const Ab = s_buf[wv][slot_on ? slot : 0][0];
+  T* const Bb = s_buf[wv][slot_on ? slot : 0][1];
+  T* const Cb = s_buf[wv][slot_on ? slot : 0][2];
+
+  // lane roles (see the file head); quadrature / mixed lines are numbered
+  // l = sl + 64 rp, rp < LPL
+  const bool r_nod = slot_on && sl < ND * ND;
+  const int ni = sl / ND, nj = sl % ND;
+  auto q_on = [&](int rp) { return slot_on && sl + 64 * rp < NQ2; };
+  auto qa_of = [&](int rp) { return (sl + 64 * rp) / NQ; };
+  auto qb_of = [&](int rp) { return (sl + 64 * rp) % NQ; };
+
+  T beta = T(0), xalpha = T(0);
+  if constexpr (MODE == kDofCG) {
+    if (A.beta_num >= 0) beta = static_cast<T>(A.scal[A.beta_num] / A.scal[A.beta_den]);
+    if (A.xa_num >= 0) xalpha = static_cast<T>(A.scal[A.xa_num] / A.scal[A.xa_den]);
   }
-  const bool bc = f & 1u;
-  if (active) sm.s0[cs][q] = (is_dof && !bc) ? u[dof] : T(0);
-  if constexpr (GEOM == kGeomOTF) {
-    if (active && q < 24 && valid) {
-      const int v = q / 3, d = q % 3;
-      sm.X[cs][v][d] = coords[3 * static_cast<int64_t>(cverts[cell * 8 + v]) + d];
+  double pap = 0.0;
+
+  // 1D tables: wave-uniform scalar loads from the operator's device buffer.
+  // Each row is read through a pointer laundered with the result of the row
+  // two before it, so the loads stream with the FMAs instead of being hoisted
+  // out of the cell loop (all tables at once would overflow the SGPR file and
+  // spill to VGPR lanes).
+  typedef const __attribute__((address_space(4))) T CT;
+  constexpr int OFF_D = NQ * ND, OFF_QP = OFF_D + NQ * NQ, OFF_W = OFF_QP + NQ;
+  CT* const tab0 = (CT*)A.tab;  // NOLINT: address-space cast (as in lap_fused5.h)
+  T ldep1 = T(0), ldep2 = T(0);
+  auto lrow = [&]() -> CT* {
+    CT* p = tab0;
+    asm volatile("" : "+s"(p) : "v"(ldep2));
+    return p;
+  };
+  auto lnext = [&](T r) {
+    ldep2 = ldep1;
+    ldep1 = r;
+  };
+
+  // XCD-aware bijective block remap: consecutive cell chunks on one XCD (its
+  // L2 then holds the dofs neighbouring cells share)
+  const int nblk = gridDim.x, ob = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = ob % 8;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + ob / 8;
+  const int c_beg = bid * A.cells_per_block;
+  const int c_end = min(c_beg + A.cells_per_block, A.ncl);
+
+  // Range-checked buffer descriptors of the gathered / scattered vectors: an
+  // offset past the range loads 0 and drops a store, so masked lanes (no
+  // cell, not a writer, Dirichlet) need no branch and every load of a cell
+  // issues back to back (a branch around a load makes the waitcnt pass fall
+  // back to vmcnt(0), which would wait for the prefetched G as well).
+  constexpr unsigned kOOB = 0xfffffff0u;
+  const unsigned vbytes = static_cast<unsigned>(A.nvec * sizeof(T));
+  auto rsrc = [](const void* ptr, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), 0, static_cast<int>(bytes),
+                                             0x00020000);
+  };
+  const auto rs_u = rsrc(A.u, vbytes), rs_f = rsrc(A.flags, static_cast<unsigned>(A.nvec));
+  const auto rs_po = rsrc(MODE == kDofCG ? A.pold : A.u, vbytes);
+  const auto rs_pn = rsrc(MODE == kDofCG ? A.pnew : A.y, MODE == kDofCG ? vbytes : 0u);
+  const auto rs_x = rsrc(MODE == kDofCG ? A.x : A.y, MODE == kDofCG ? vbytes : 0u);
+  const auto rs_y = rsrc(A.y, vbytes);
+  // per-cell coefficient: range 0 when there is none (the load returns 0)
+  const auto rs_kc = rsrc(A.kc ? A.kc : A.y, A.kc ? 0x7ffffff0u : 0u);
+  auto ldv = [](__amdgpu_buffer_rsrc_t r, unsigned off) -> T {
+    if constexpr (sizeof(T) == 8)
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    else
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+  };
+  auto stv = [](__amdgpu_buffer_rsrc_t r, unsigned off, T v) {
+    if constexpr (sizeof(T) == 8)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bdx_u32x2, v), r, off, 0, 0);
+    else
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+  };
+
+  // ---- software pipeline over this wave's cells (iteration j: list index
+  // li = first + STEP j).  Cell ids come from a per-wave LDS ring filled one
+  // block of IB iterations ahead (no global-load latency on the id), each
+  // iteration issues the next cell's gathers and stored G and the dofs of the
+  // cell after it, and the loop is unrolled by two with alternating dof /
+  // vertex register sets, so no register holding an in-flight load is ever
+  // copied (a copy would make the wave wait for it at the loop latch).
+  constexpr int STEP = S::WAVES * CPW;
+  constexpr int IB = 64 / CPW;               // iterations per id block
+  constexpr int XPL = (24 + NQ2 - 1) / NQ2;  // vertex coordinates per lane (OTF)
+  const int first = c_beg + wv * CPW + slot;
+  const int last_li = c_end - 1;
+  const int wbase = c_beg + wv * CPW;  // list index of (iteration 0, slot 0)
+  const int id_lane = (lane / CPW) * STEP + lane % CPW;  // this lane's entry of a block
+  auto id_load = [&](int blk) -> int {
+    const int li = wbase + blk * IB * STEP + id_lane;
+    return A.cells[li < last_li ? li : last_li];
+  };
+  auto id_put = [&](int blk, int v) {
+    if (lane < IB * CPW) s_ids[wv][blk & 1][lane] = v;
+  };
+  auto cell_of = [&](int j) -> int { return s_ids[wv][(j / IB) & 1][(j % IB) * CPW + (slot_on ? slot : 0)]; };
+  const int nodoff = r_nod ? (ni * ND + nj) * ND : 0;
+  auto load_dofs = [&](int c32, int (&d)[ND]) {
+    const int64_t c = c32;
+#pragma unroll
+    for (int k = 0; k < ND; ++k) d[k] = A.cdofs[c * ND3 + nodoff + k];
+  };
+  auto load_verts = [&](int c32, int (&vx)[XPL]) {
+    const int64_t c = c32;
+#pragma unroll
+    for (int e = 0; e < XPL; ++e) {
+      const int x = sl + NQ2 * e;
+      vx[e] = GEOM == kGeomOTF ? A.cverts[c * 8 + (x < 24 ? x / 3 : 0)] : 0;
     }
+  };
+  struct Gather {
+    T u[ND], po[ND], x[ND], X[XPL];
+    unsigned f[ND];
+    T kc;
+  };
+  auto gather = [&](const int (&d)[ND], const int (&vx)[XPL], int c32, bool ok, Gather& g) {
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      const unsigned dd = static_cast<unsigned>(d[k] & 0x7fffffff);
+      const bool on = ok & r_nod;
+      g.f[k] = __builtin_amdgcn_raw_buffer_load_b8(rs_f, on ? dd : kOOB, 0, 0);
+      g.u[k] = ldv(rs_u, on ? dd * sizeof(T) : kOOB);
+      g.po[k] = MODE == kDofCG ? ldv(rs_po, on ? dd * sizeof(T) : kOOB) : T(0);
+      const bool xw = on & (d[k] < 0) & (MODE == kDofCG) & (A.xa_num >= 0);
+      g.x[k] = MODE == kDofCG ? ldv(rs_x, xw ? dd * sizeof(T) : kOOB) : T(0);
+    }
+#pragma unroll
+    for (int e = 0; e < XPL; ++e) {
+      const int x = sl + NQ2 * e;
+      g.X[e] = GEOM == kGeomOTF ? A.coords[3 * static_cast<int64_t>(vx[e]) + (x < 24 ? x % 3 : 0)]
+                                : T(0);
+    }
+    g.kc = ldv(rs_kc, static_cast<unsigned>(c32) * sizeof(T));
+  };
+  T Gr[LPL][GPREF ? 6 * NQ : 1];
+  auto load_G = [&](int c32) {
+    if constexpr (GPREF) {
+      const T* Gc = A.G + static_cast<int64_t>(c32) * 6 * NQ3;
+#pragma unroll
+      for (int rp = 0; rp < LPL; ++rp)
+#pragma unroll
+        for (int qx = 0; qx < NQ; ++qx)
+#pragma unroll
+          for (int k = 0; k < 6; ++k)
+            Gr[rp][k * NQ + qx] = Gc[k * NQ3 + qx * NQ2 + (q_on(rp) ? sl + 64 * rp : 0)];
+    }
+  };
+
+  const bool wave_on = wbase < c_end;
+  const int nit = wave_on ? (c_end - wbase + STEP - 1) / STEP : 0;  // iterations of this wave
+  int dA[ND], dB[ND], vA[XPL], vB[XPL];
+  int cell_cur = 0, id_next = 0;
+  Gather gc;
+  if (wave_on) {
+    id_put(0, id_load(0));
+    dof_wave_sync();
+    cell_cur = cell_of(0);
+    load_dofs(cell_cur, dA);
+    load_verts(cell_cur, vA);
+    gather(dA, vA, cell_cur, slot_on && first < c_end, gc);
+    load_G(cell_cur);
+    load_dofs(cell_of(1), dB);
+    load_verts(cell_of(1), vB);
   }
-  __syncthreads();
-  const T* Gc = (GEOM == kGeomStored && valid) ? G + cell * 6 * nq3 : G;
-  const T kap = (kc && valid) ? kc[cell] : kappa;
-  const T ye = v1_core<T, ND, NQ, kModeStiffness, GEOM>(sm, tb, cs, q, active, valid, Gc, kap);
-  if (is_dof) {
-    if (!bc)
-      atomicAdd(y + dof, ye);
-    else if (f & 2u)
-      y[dof] = u[dof];  // Dirichlet identity row (owned copy only)
+
+  // one cell of the pipeline: (dc, vc) hold its dofs / vertices (landed),
+  // (dn, vn) the next cell's (in flight); the advance overwrites (dc, vc)
+  // with the dofs of the cell after next
+  auto iter = [&](int j, int (&dc)[ND], int (&dn)[ND], int (&vc)[XPL], int (&vn)[XPL])
+      __attribute__((always_inline)) {
+    const int li = first + j * STEP;
+    const bool valid = slot_on && li < c_end;
+    const int64_t cell = cell_cur;
+    (void)vc;
+    // id ring: block b + 1 is loaded when block b starts and written to the
+    // ring half a block later (before any cell_of reaches into it)
+    if (j % IB == 0) id_next = id_load(j / IB + 1);
+    if (j % IB == IB / 2) id_put(j / IB + 1, id_next);
+    const T kap = A.kc ? gc.kc : A.kappa;
+
+    // ---- the gathered z-line of lane (i, j): p = r + beta p_old (CG), the
+    // writer's p / lagged x stores, Dirichlet identity rows
+    int dof[ND];
+    unsigned fl[ND];
+    T ue[ND];
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      dof[k] = dc[k];
+      const int d = dof[k] & 0x7fffffff;
+      const bool on = valid && r_nod;
+      const bool wr = on && dof[k] < 0;
+      fl[k] = (on ? gc.f[k] : 0u) | (wr ? 4u : 0u);
+      T v = gc.u[k];
+      if constexpr (MODE == kDofCG) {
+        v = gc.u[k] + beta * gc.po[k];
+        stv(rs_pn, wr ? static_cast<unsigned>(d) * sizeof(T) : kOOB, v);
+        stv(rs_x, (wr && A.xa_num >= 0) ? static_cast<unsigned>(d) * sizeof(T) : kOOB,
+            gc.x[k] + xalpha * gc.po[k]);
+      }
+      const bool bc = fl[k] & 1u;
+      const bool idrow = (fl[k] & 7u) == 7u;  // Dirichlet, owned, writer
+      stv(rs_y, idrow ? static_cast<unsigned>(d) * sizeof(T) : kOOB, v);
+      if constexpr (MODE == kDofCG) {
+        if (idrow) pap += static_cast<double>(v) * static_cast<double>(v);
+      }
+      ue[k] = bc ? T(0) : v;  // zero column
+    }
+    if constexpr (GEOM == kGeomOTF) {
+#pragma unroll
+      for (int e = 0; e < XPL; ++e) {
+        const int x = sl + NQ2 * e;
+        if (slot_on && x < 24) s_X[wv][slot][x] = gc.X[e];
+      }
+    }
+
+    // ---- interpolation to the quadrature points: z (nodal lanes), y (mixed), x (quad)
+    T U[LPL][NQ];
+    if constexpr (IDENT) {
+      if (r_nod) {
+#pragma unroll
+        for (int k = 0; k < ND; ++k) Ab[(ni * NQ + nj) * NQP + k] = ue[k];
+      }
+      dof_wave_sync();
+#pragma unroll
+      for (int rp = 0; rp < LPL; ++rp)
+#pragma unroll
+        for (int qx = 0; qx < NQ; ++qx)
+          U[rp][qx] = q_on(rp) ? Ab[(qx * NQ + qa_of(rp)) * NQP + qb_of(rp)] : T(0);
+    } else {
+      if (r_nod) {
+#pragma unroll
+        for (int qz = 0; qz < NQ; ++qz) {
+          CT* t = lrow();
+          T s = T(0);
+#pragma unroll
+          for (int k = 0; k < ND; ++k) s += t[qz * ND + k] * ue[k];
+          lnext(s);
+          Ab[(ni * NQ + nj) * NQP + qz] = s;
+        }
+      }
+      dof_wave_sync();
+#pragma unroll
+      for (int rp = 0; rp < (ND * NQ + 63) / 64; ++rp) {
+        const int l = sl + 64 * rp, mi = l / NQ, mq = l % NQ;
+        if (slot_on && l < ND * NQ) {  // mixed lane (i, qz)
+          T in[ND];
+#pragma unroll
+          for (int j = 0; j < ND; ++j) in[j] = Ab[(mi * NQ + j) * NQP + mq];
+#pragma unroll
+          for (int qy = 0; qy < NQ; ++qy) {
+            CT* t = lrow();
+            T s = T(0);
+#pragma unroll
+            for (int j = 0; j < ND; ++j) s += t[qy * ND + j] * in[j];
+            lnext(s);
+            Bb[(mi * NQ + qy) * NQP + mq] = s;
+          }
+        }
+      }
+      dof_wave_sync();
+#pragma unroll
+      for (int rp = 0; rp < LPL; ++rp) {
+        T in[ND];
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          in[i] = q_on(rp) ? Bb[(i * NQ + qa_of(rp)) * NQP + qb_of(rp)] : T(0);
+#pragma unroll
+        for (int qx = 0; qx < NQ; ++qx) {
+          CT* t = lrow();
+          T s = T(0);
+#pragma unroll
+          for (int i = 0; i < ND; ++i) s += t[qx * ND + i] * in[i];
+          lnext(s);
+          U[rp][qx] = s;
+        }
+        if (q_on(rp)) {
+#pragma unroll
+          for (int qx = 0; qx < NQ; ++qx) Ab[(qx * NQ + qa_of(rp)) * NQP + qb_of(rp)] = U[rp][qx];
+        }
+      }
+      dof_wave_sync();
+    }
+
+    // ---- reference gradient: x in registers, y / z by the transposed lane roles
+#pragma unroll
+    for (int rp = 0; rp < LPL; ++rp) {
+      if (!q_on(rp)) continue;
+      const int a = qa_of(rp), b = qb_of(rp);
+      T in[NQ], o[NQ];
+#pragma unroll
+      for (int m = 0; m < NQ; ++m) in[m] = Ab[(a * NQ + m) * NQP + b];  // y-line (qx, qz)
+#pragma unroll
+      for (int qy = 0; qy < NQ; ++qy) {
+        CT* t = lrow();
+        T s = T(0);
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) s += t[OFF_D + qy * NQ + m] * in[m];
+        lnext(s);
+        o[qy] = s;
+      }
+#pragma unroll
+      for (int qy = 0; qy < NQ; ++qy) Bb[(a * NQ + qy) * NQP + b] = o[qy];
+#pragma unroll
+      for (int m = 0; m < NQ; ++m) in[m] = Ab[(a * NQ + b) * NQP + m];  // z-line (qx, qy)
+#pragma unroll
+      for (int qz = 0; qz < NQ; ++qz) {
+        CT* t = lrow();
+        T s = T(0);
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) s += t[OFF_D + qz * NQ + m] * in[m];
+        lnext(s);
+        o[qz] = s;
+      }
+#pragma unroll
+      for (int qz = 0; qz < NQ; ++qz) Cb[(a * NQ + b) * NQP + qz] = o[qz];
+    }
+    dof_wave_sync();
+
+    // ---- F = kappa G grad U at the points of this lane's x-lines (qy, qz) = (a, b)
+    T Fx[LPL][NQ];
+    if constexpr (GEOM == kGeomOTF) {
+      T Xc[8][3];
+#pragma unroll
+      for (int v = 0; v < 8; ++v)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) Xc[v][d] = s_X[wv][slot_on ? slot : 0][v * 3 + d];
+#pragma unroll
+      for (int rp = 0; rp < LPL; ++rp) {
+        const int a = qa_of(rp), b = qb_of(rp);
+#pragma unroll
+        for (int qx = 0; qx < NQ; ++qx) {
+          Fx[rp][qx] = T(0);
+          if (!q_on(rp)) continue;
+          CT* t = lrow();
+          T gx = T(0);
+#pragma unroll
+          for (int m = 0; m < NQ; ++m) gx += t[OFF_D + qx * NQ + m] * U[rp][m];
+          lnext(gx);
+          const T gy = Bb[(qx * NQ + a) * NQP + b], gz = Cb[(qx * NQ + a) * NQP + b];
+          T Gd[6];
+          CT* tq = lrow();
+          geometry_G<T>(Xc, tq[OFF_QP + qx], tq[OFF_QP + a], tq[OFF_QP + b],
+                        tq[OFF_W + qx] * tq[OFF_W + a] * tq[OFF_W + b], Gd);
+          const T kv = valid ? kap : T(0);
+          Fx[rp][qx] = kv * (Gd[0] * gx + Gd[1] * gy + Gd[2] * gz);
+          Bb[(qx * NQ + a) * NQP + b] = kv * (Gd[1] * gx + Gd[3] * gy + Gd[4] * gz);
+          Cb[(qx * NQ + a) * NQP + b] = kv * (Gd[2] * gx + Gd[4] * gy + Gd[5] * gz);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int rp = 0; rp < LPL; ++rp) {
+        const int a = qa_of(rp), b = qb_of(rp);
+#pragma unroll
+        for (int qx = 0; qx < NQ; ++qx) {
+          Fx[rp][qx] = T(0);
+          if (!q_on(rp)) continue;
+          CT* t = lrow();
+          T gx = T(0);
+#pragma unroll
+          for (int m = 0; m < NQ; ++m) gx += t[OFF_D + qx * NQ + m] * U[rp][m];
+          lnext(gx);
+          const T gy = Bb[(qx * NQ + a) * NQP + b], gz = Cb[(qx * NQ + a) * NQP + b];
+          T Gd[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            if constexpr (GPREF)
+              Gd[k] = Gr[rp][k * NQ + qx];
+            else
+              Gd[k] = A.G[cell * 6 * NQ3 + k * NQ3 + qx * NQ2 + sl + 64 * rp];
+          }
+          Fx[rp][qx] = kap * (Gd[0] * gx + Gd[1] * gy + Gd[2] * gz);
+          Bb[(qx * NQ + a) * NQP + b] = kap * (Gd[1] * gx + Gd[3] * gy + Gd[4] * gz);
+          Cb[(qx * NQ + a) * NQP + b] = kap * (Gd[2] * gx + Gd[4] * gy + Gd[5] * gz);
+        }
+      }
+    }
+    dof_wave_sync();
+
+    // ---- transposed gradient: y / z lines by the transposed lanes (in place:
+    // every line is read whole before it is rewritten, lines are disjoint)
+#pragma unroll
+    for (int rp = 0; rp < LPL; ++rp) {
+      if (!q_on(rp)) continue;
+      const int a = qa_of(rp), b = qb_of(rp);
+      T in[NQ], o[NQ];
+#pragma unroll
+      for (int m = 0; m < NQ; ++m) in[m] = Bb[(a * NQ + m) * NQP + b];
+#pragma unroll
+      for (int qy = 0; qy < NQ; ++qy) {
+        CT* t = lrow();
+        T s = T(0);
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) s += t[OFF_D + m * NQ + qy] * in[m];
+        lnext(s);
+        o[qy] = s;
+      }
+#pragma unroll
+      for (int qy = 0; qy < NQ; ++qy) Bb[(a * NQ + qy) * NQP + b] = o[qy];
+#pragma unroll
+      for (int m = 0; m < NQ; ++m) in[m] = Cb[(a * NQ + b) * NQP + m];
+#pragma unroll
+      for (int qz = 0; qz < NQ; ++qz) {
+        CT* t = lrow();
+        T s = T(0);
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) s += t[OFF_D + m * NQ + qz] * in[m];
+        lnext(s);
+        o[qz] = s;
+      }
+#pragma unroll
+      for (int qz = 0; qz < NQ; ++qz) Cb[(a * NQ + b) * NQP + qz] = o[qz];
+    }
+    dof_wave_sync();
+    T R[LPL][NQ];
+#pragma unroll
+    for (int rp = 0; rp < LPL; ++rp) {
+      const int a = qa_of(rp), b = qb_of(rp);
+#pragma unroll
+      for (int qx = 0; qx < NQ; ++qx) {
+        CT* t = lrow();
+        T s = q_on(rp) ? Bb[(qx * NQ + a) * NQP + b] + Cb[(qx * NQ + a) * NQP + b] : T(0);
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) s += t[OFF_D + m * NQ + qx] * Fx[rp][m];
+        lnext(s);
+        R[rp][qx] = s;
+      }
+    }
+
+    // ---- transposed interpolation: x (quad lanes), y (mixed), z (nodal lanes)
+    T ye[ND];
+#pragma unroll
+    for (int k = 0; k < ND; ++k) ye[k] = T(0);
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int rp = 0; rp < LPL; ++rp) {
+        if (!q_on(rp)) continue;
+#pragma unroll
+        for (int qx = 0; qx < NQ; ++qx) Ab[(qx * NQ + qa_of(rp)) * NQP + qb_of(rp)] = R[rp][qx];
+      }
+      dof_wave_sync();
+      if (r_nod) {
+#pragma unroll
+        for (int k = 0; k < ND; ++k) ye[k] = Ab[(ni * NQ + nj) * NQP + k];
+      }
+    } else {
+#pragma unroll
+      for (int rp = 0; rp < LPL; ++rp) {
+        if (!q_on(rp)) continue;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+          CT* t = lrow();
+          T s = T(0);
+#pragma unroll
+          for (int qx = 0; qx < NQ; ++qx) s += t[qx * ND + i] * R[rp][qx];
+          lnext(s);
+          Ab[(i * NQ + qa_of(rp)) * NQP + qb_of(rp)] = s;
+        }
+      }
+      dof_wave_sync();
+#pragma unroll
+      for (int rp = 0; rp < (ND * NQ + 63) / 64; ++rp) {
+        const int l = sl + 64 * rp, mi = l / NQ, mq = l % NQ;
+        if (slot_on && l < ND * NQ) {  // mixed lane (i, qz)
+          T in[NQ];
+#pragma unroll
+          for (int qy = 0; qy < NQ; ++qy) in[qy] = Ab[(mi * NQ + qy) * NQP + mq];
+#pragma unroll
+          for (int j = 0; j < ND; ++j) {
+            CT* t = lrow();
+            T s = T(0);
+#pragma unroll
+            for (int qy = 0; qy < NQ; ++qy) s += t[qy * ND + j] * in[qy];
+            lnext(s);
+            Bb[(mi * NQ + j) * NQP + mq] = s;
+          }
+        }
+      }
+      dof_wave_sync();
+      if (r_nod) {
+        T in[NQ];
+#pragma unroll
+        for (int qz = 0; qz < NQ; ++qz) in[qz] = Bb[(ni * NQ + nj) * NQP + qz];
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+          CT* t = lrow();
+          T s = T(0);
+#pragma unroll
+          for (int qz = 0; qz < NQ; ++qz) s += t[qz * ND + k] * in[qz];
+          lnext(s);
+          ye[k] = s;
+        }
+      }
+    }
+
+    // ---- advance the pipeline: the next cell's gathers and G, the dofs of
+    // the one after (issued before this cell's atomics, which need no wait)
+    {
+      dof_wave_sync();  // the id ring entry of j + 1 / j + 2 is visible
+      const int cn = cell_of(j + 1), cnn = cell_of(j + 2);
+      gather(dn, vn, cn, slot_on && li + STEP < c_end, gc);
+      load_G(cn);
+      load_dofs(cnn, dc);
+      load_verts(cnn, vc);
+      cell_cur = cn;
+    }
+
+    // ---- scatter-add (non-Dirichlet dofs) and the element dot p_e . (A_e p_e)
+    if (r_nod && valid) {
+#pragma unroll
+      for (int k = 0; k < ND; ++k) {
+        if (fl[k] & 1u) continue;
+        const int d = dof[k] & 0x7fffffff;
+        atomicAdd(A.y + d, ye[k]);
+        if constexpr (MODE == kDofCG) pap += static_cast<double>(ue[k]) * static_cast<double>(ye[k]);
+      }
+    }
+    dof_wave_sync();  // the next cell reuses the wave's buffers
+  };
+  for (int j = 0; j < nit; j += 2) {
+    iter(j, dA, dB, vA, vB);
+    if (j + 1 < nit) iter(j + 1, dB, dA, vB, vA);
+  }
+  if constexpr (MODE == kDofCG) {
+    const double t = block_sum(pap, s_red);
+    if (tid == 0) A.partials[bid] = t;
   }
 }
 
@@ -93,19 +662,92 @@ __global__ void __launch_bounds__(256)
   for (int k = 0; k < 6; ++k) G[(cell * 6 + k) * nq3 + q] = Gd[k];
 }
 
+// Writer designation: the first occurrence (in launch order: the cell list
+// `cells`, position p = list index * ND^3 + local dof) of every dof.
+static __global__ void __launch_bounds__(256)
+    dofmap_first_kernel(const int* __restrict__ cells, int ncl, const int* __restrict__ cdofs,
+                        int nd3, int pos0, unsigned* __restrict__ first) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<int64_t>(ncl) * nd3) return;
+  const int64_t li = t / nd3;
+  const int loc = static_cast<int>(t - li * nd3);
+  const int d = cdofs[static_cast<int64_t>(cells[li]) * nd3 + loc] & 0x7fffffff;
+  atomicMin(first + d, static_cast<unsigned>(pos0 + t));
+}
+static __global__ void __launch_bounds__(256)
+    dofmap_mark_kernel(const int* __restrict__ cells, int ncl, int* __restrict__ cdofs, int nd3,
+                       int pos0, const unsigned* __restrict__ first) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<int64_t>(ncl) * nd3) return;
+  const int64_t li = t / nd3;
+  const int loc = static_cast<int>(t - li * nd3);
+  int* e = cdofs + static_cast<int64_t>(cells[li]) * nd3 + loc;
+  const int d = *e & 0x7fffffff;
+  *e = (first[d] == static_cast<unsigned>(pos0 + t)) ? (d | static_cast<int>(0x80000000u)) : d;
+}
+
+// CG update of the dofmap path: alpha = s[rn] / s[pap]; r -= alpha y over
+// every local dof, r.r over the owned ones, y = 0 for the next operator.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    dofmap_cg_update_kernel(int64_t n, const unsigned char* __restrict__ flags, T* __restrict__ r,
+                            T* __restrict__ y, const double* __restrict__ scal, int rn_slot,
+                            int pap_slot, double* __restrict__ partials) {
+  __shared__ double lds[16];
+  const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
+  double acc = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const T rn = r[i] - alpha * y[i];
+    r[i] = rn;
+    y[i] = T(0);
+    if (flags[i] & 2u) acc += static_cast<double>(rn) * static_cast<double>(rn);
+  }
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+// x += (s[num] / s[den]) p over every local dof (the lagged x update's flush)
+template <typename T>
+__global__ void __launch_bounds__(256)
+    dofmap_xflush_kernel(int64_t n, T* __restrict__ x, const T* __restrict__ p,
+                         const double* __restrict__ scal, int num, int den) {
+  const T a = static_cast<T>(scal[num] / scal[den]);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    x[i] += a * p[i];
+}
+
+constexpr int kDofMaxBlocks = 16384;  // partials per launch (<= bdx_hip_partials_size / 2)
+
+// Blocks of a launch over ncl cells: whole waves of cells per block, at most
+// kDofMaxBlocks blocks (each marches a contiguous chunk of the cell list).
+template <int NQ>
+inline int dofmap_blocks(int ncl, int* cells_per_block) {
+  constexpr int step = DofShape<NQ>::WAVES * DofShape<NQ>::CPW;
+  int64_t nb = (static_cast<int64_t>(ncl) + step - 1) / step;
+  int64_t cpb = step;
+  if (nb > kDofMaxBlocks) {
+    cpb = ((static_cast<int64_t>(ncl) + kDofMaxBlocks - 1) / kDofMaxBlocks + step - 1) / step * step;
+    nb = (ncl + cpb - 1) / cpb;
+  }
+  *cells_per_block = static_cast<int>(cpb);
+  return static_cast<int>(nb);
+}
+
 template <typename T, int ND, int NQ>
-int launch_dofmap(int geom, const int* cells, int ncl, const int* cdofs, const int* cverts,
-                  const T* coords, const unsigned char* flags, const OpTables<T>& tb, const T* G,
-                  T kappa, const T* kc, const T* u, T* y, hipStream_t st) {
-  if (ncl <= 0) return 0;
-  constexpr int cpb = V1Shape<NQ>::cpb;
-  const int nblk = (ncl + cpb - 1) / cpb;
+int launch_dofmap(int geom, int mode, DofArgs<T> a, int* nblocks, hipStream_t st) {
+  *nblocks = 0;
+  if (a.ncl <= 0) return 0;
+  const int nb = dofmap_blocks<NQ>(a.ncl, &a.cells_per_block);
+  *nblocks = nb;
+  constexpr int NT = DofShape<NQ>::NT;
+#define BDX_DL(G, M) lap_dofmap_kernel<T, ND, NQ, G, M><<<nb, NT, 0, st>>>(a)
   if (geom == kGeomStored)
-    lap_dofmap_kernel<T, ND, NQ, kGeomStored><<<nblk, V1Shape<NQ>::threads, 0, st>>>(
-        cells, ncl, cdofs, cverts, coords, flags, tb, G, kappa, kc, u, y);
+    (mode == kDofCG) ? BDX_DL(kGeomStored, kDofCG) : BDX_DL(kGeomStored, kDofAction);
   else
-    lap_dofmap_kernel<T, ND, NQ, kGeomOTF><<<nblk, V1Shape<NQ>::threads, 0, st>>>(
-        cells, ncl, cdofs, cverts, coords, flags, tb, G, kappa, kc, u, y);
+    (mode == kDofCG) ? BDX_DL(kGeomOTF, kDofCG) : BDX_DL(kGeomOTF, kDofAction);
+#undef BDX_DL
   return static_cast<int>(hipGetLastError());
 }
 
@@ -122,16 +764,20 @@ int launch_dofmap_geometry(int ncells, const int* cverts, const T* coords, const
   return static_cast<int>(hipGetLastError());
 }
 
+// apply: mode 0 = action (u -> y += A u), 1 = CG operator (u = r); returns the
+// number of p.Ap partials written at partials (CG) in *nblocks.
 #define BDX_DOFMAP_API(T, SUF)                                                                    \
-  extern "C" int bdx_dofmap_apply_##SUF(int P, int nq, int geom, const double* phi0,             \
-                                        const double* dphi1, const double* wts,                   \
-                                        const double* qpts, int identity, const int* cells,       \
-                                        int ncl, const int* cdofs, const int* cverts,             \
-                                        const T* coords, const unsigned char* flags, const T* G,  \
-                                        double kappa, const T* kc, const T* u, T* y,              \
-                                        hipStream_t st) {                                         \
-    const OpTables<T> tb = make_op_tables<T>(P + 1, nq, phi0, dphi1, wts, qpts, identity);       \
-    const T k = static_cast<T>(kappa);                                                            \
+  extern "C" int bdx_dofmap_apply_##SUF(                                                          \
+      int P, int nq, int geom, int mode, const T* tab, const int* cells, int ncl, int64_t nvec,   \
+      const int* cdofs, const int* cverts, const T* coords, const unsigned char* flags,           \
+      const T* G, double kappa, const T* kc, const T* u, const T* pold, T* pnew, T* x, T* y,      \
+      const double* scal, int beta_num, int beta_den, int xa_num, int xa_den, double* partials,   \
+      int* nblocks, hipStream_t st) {                                                             \
+    DofArgs<T> a{cells, ncl, 0, nvec, cdofs, cverts, coords, flags, G, tab,                       \
+                 static_cast<T>(kappa), kc, u, pold, pnew, x, y, scal, beta_num, beta_den,        \
+                 xa_num, xa_den, partials};                                                       \
+    if (nvec * static_cast<int64_t>(sizeof(T)) >= 0xfffffff0LL)                                   \
+      return static_cast<int>(hipErrorInvalidValue);                                              \
     switch (P * 16 + nq) {                                                                        \
       BDX_DOFMAP_CASE(T, 1)                                                                       \
       BDX_DOFMAP_CASE(T, 2)                                                                       \
@@ -159,12 +805,27 @@ int launch_dofmap_geometry(int ncells, const int* cverts, const T* coords, const
       case 9: return launch_dofmap_geometry<T, 9>(ncells, cverts, coords, tb, G, st);             \
     }                                                                                             \
     return static_cast<int>(hipErrorInvalidValue);                                                \
+  }                                                                                               \
+  extern "C" int bdx_dofmap_cg_update_##SUF(int64_t n, const unsigned char* flags, T* r, T* y,    \
+                                            const double* scal, int rn_slot, int pap_slot,        \
+                                            double* partials, int* nblocks, hipStream_t st) {     \
+    const int64_t want = (n + 1023) / 1024;                                                       \
+    const int g = static_cast<int>(want < kDofMaxBlocks ? (want > 0 ? want : 1) : kDofMaxBlocks); \
+    dofmap_cg_update_kernel<T><<<g, 256, 0, st>>>(n, flags, r, y, scal, rn_slot, pap_slot,        \
+                                                  partials);                                      \
+    *nblocks = g;                                                                                 \
+    return static_cast<int>(hipGetLastError());                                                   \
+  }                                                                                               \
+  extern "C" int bdx_dofmap_xflush_##SUF(int64_t n, T* x, const T* p, const double* scal,         \
+                                         int num, int den, hipStream_t st) {                      \
+    const int64_t want = (n + 1023) / 1024;                                                       \
+    const int g = static_cast<int>(want < kDofMaxBlocks ? (want > 0 ? want : 1) : kDofMaxBlocks); \
+    dofmap_xflush_kernel<T><<<g, 256, 0, st>>>(n, x, p, scal, num, den);                          \
+    return static_cast<int>(hipGetLastError());                                                   \
   }
 
 #define BDX_DOFMAP_CASE(T, PP)                                                                    \
   case PP * 16 + PP + 1:                                                                          \
-    return launch_dofmap<T, PP + 1, PP + 1>(geom, cells, ncl, cdofs, cverts, coords, flags, tb,   \
-                                            G, k, kc, u, y, st);                                  \
+    return launch_dofmap<T, PP + 1, PP + 1>(geom, mode, a, nblocks, st);                          \
   case PP * 16 + PP + 2:                                                                          \
-    return launch_dofmap<T, PP + 1, PP + 2>(geom, cells, ncl, cdofs, cverts, coords, flags, tb,   \
-                                            G, k, kc, u, y, st);
+    return launch_dofmap<T, PP + 1, PP + 2>(geom, mode, a, nblocks, st);

@@ -6,19 +6,20 @@
 // interior-cell kernel (src/laplacian.hpp:281-349).  This runtime owns one
 // rank's iteration on two HIP streams, every scalar device-resident:
 //
-//   compute stream                         comm stream
-//   --------------                         -----------
-//   fused op, interior tiles A      ||     pack r faces -> RCCL send/recv -> unpack ghosts
-//   fused op, ghost-touching tiles  (after the forward exchange)
-//   ghost-plane finalize
-//   fused op, interior tiles B      ||     pack y ghosts -> RCCL send/recv
-//   unpack-add y faces (after the reverse exchange)
+//   compute stream                     comm stream
+//   --------------                     -----------
+//   fused op, all interior tiles  ||   pack r faces -> RCCL send/recv -> unpack ghosts
+//                                 ||   fused op, ghost-touching tiles (last row / column)
+//                                 ||   ghost-plane finalize
+//                                 ||   pack y ghosts -> RCCL send/recv
+//   (join) unpack-add y faces
 //   reduce(p.Ap) -> all-reduce -> r update (+ r.r) -> all-reduce
 //
 // The tile split needs an unsplit march axis (x): the partition keeps x whole
 // on the GPU platform (fem/mesh.py partition_grid), so only the last (y, z)
 // tile row / column touches a ghost plane and every other tile can run while
-// the halo is in flight; both exchanges are hidden.  Otherwise (x split, one
+// the halo is in flight.  The whole comm-stream chain -- both exchanges and
+// the small boundary launches -- runs under the one large interior launch.  Otherwise (x split, one
 // rank) the iteration runs serially on the compute stream.  Halos are
 // grouped RCCL point-to-point sends/receives with the <= 7 neighbours over
 // xGMI; the steady-state iterations (two parities: the p buffers and the r.r
@@ -392,12 +393,12 @@ enum Mark {
   kMStart = 0,   // compute stream: iteration start
   kMFwdBeg,      // comm stream: forward exchange start
   kMFwdEnd,      // comm stream: ghost planes of r unpacked
-  kMOpA,         // compute: interior tiles A done (serial: the whole operator)
-  kMBnd,         // compute: ghost-touching tiles + ghost finalize done
+  kMOpA,         // compute: interior tiles done (serial: the whole operator)
+  kMBnd,         // comm: ghost-touching tiles + ghost finalize done
   kMRevBeg,      // comm: reverse exchange start
-  kMRevEnd,      // comm: reverse exchange done (serial: + unpack-add)
-  kMOpB,         // compute: interior tiles B done
-  kMPap,         // compute: unpack-add + reduce + all-reduce(p.Ap) done
+  kMRevEnd,      // comm: reverse send done (serial: + unpack-add)
+  kMJoin,        // compute: comm stream joined, received sums added
+  kMPap,         // compute: reduce + all-reduce(p.Ap) done
   kMUpd,         // compute: r update (+ r.r) done
   kMEnd,         // compute: all-reduce(r.r) done
   kNMarks
@@ -421,8 +422,7 @@ struct CGRuntime {
   // default stream torch may be using); ordered against the caller's stream
   // `ext` with events at the start and end of every iterate()
   hipStream_t st = nullptr, cs = nullptr, ext = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_fwd = nullptr,
-             ev_bnd = nullptr, ev_rev = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_rev = nullptr;
   ApplyFn<T> apply = nullptr;
   std::vector<T> tabs_host;
   const T* tabs = nullptr;  // host copy (fused2-4: kernarg tables) or device buffer (fused5)
@@ -447,7 +447,7 @@ struct CGRuntime {
   std::vector<int64_t> face_cnt, face_off, ghost_cnt, ghost_off;
   // overlapped schedule: tile rectangles {ty0, ty1, tz0, tz1}
   bool split = false;
-  int rect_a[4], rect_b[4], rect_r1[4], rect_r2[4];
+  int rect_a[4], rect_r1[4], rect_r2[4];  // interior, last tile row, last tile column
   // phase profiling (eager iterations only)
   bool prof = false;
   hipEvent_t pev[kNMarks] = {};
@@ -529,28 +529,35 @@ struct CGRuntime {
     int rc;
     mark(kMStart, st);
     if (split) {
+      // Two streams (reference src/laplacian.hpp:281-349, redesigned):
+      //   cs: forward exchange -> boundary tiles (the last tile row and
+      //       column, which read the ghost planes) -> ghost-plane fold ->
+      //       reverse send;
+      //   st: every interior tile, concurrently -- the exchanges and the
+      //       small boundary launches all ride under the interior launch, so
+      //       none of them is on the critical path as long as the interior
+      //       work outlasts them;
+      //   st: wait for cs, add the received sums into the owned faces.
+      // Write sets are disjoint: a tile writes only its own nodes and its own
+      // interface partials, and the ghost-plane fold reads only partials of
+      // boundary tiles (fused_finalize_ghost_kernel).
       BDX_CHECK(hipEventRecord(ev_fork, st));
       BDX_CHECK(hipStreamWaitEvent(cs, ev_fork, 0));
       mark(kMFwdBeg, cs);
       if ((rc = halo_forward(r, cs))) return rc;
-      BDX_CHECK(hipEventRecord(ev_fwd, cs));
       mark(kMFwdEnd, cs);
-      if ((rc = op(rect_a, st))) return rc;
-      mark(kMOpA, st);
-      BDX_CHECK(hipStreamWaitEvent(st, ev_fwd, 0));
-      if ((rc = op(rect_r1, st)) || (rc = op(rect_r2, st)) || (rc = finalize_ghost(st)))
+      if ((rc = op(rect_r1, cs)) || (rc = op(rect_r2, cs)) || (rc = finalize_ghost(cs)))
         return rc;
-      BDX_CHECK(hipEventRecord(ev_bnd, st));
-      mark(kMBnd, st);
-      BDX_CHECK(hipStreamWaitEvent(cs, ev_bnd, 0));
+      mark(kMBnd, cs);
       mark(kMRevBeg, cs);
       if ((rc = halo_reverse_send(y, cs))) return rc;
       BDX_CHECK(hipEventRecord(ev_rev, cs));
       mark(kMRevEnd, cs);
-      if ((rc = op(rect_b, st))) return rc;
-      mark(kMOpB, st);
+      if ((rc = op(rect_a, st))) return rc;
+      mark(kMOpA, st);
       BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
       if ((rc = halo_reverse_add(y, st))) return rc;
+      mark(kMJoin, st);
     } else {
       mark(kMFwdBeg, st);
       if (halo && (rc = halo_forward(r, st))) return rc;
@@ -562,7 +569,7 @@ struct CGRuntime {
       mark(kMRevBeg, st);
       if (halo && ((rc = halo_reverse_send(y, st)) || (rc = halo_reverse_add(y, st)))) return rc;
       mark(kMRevEnd, st);
-      mark(kMOpB, st);
+      mark(kMJoin, st);
     }
     if ((rc = bdx_reduce_partials(partials, cfg.nblocks, scal, kPAP, st))) return rc;
     if (nranks > 1 && (rc = tr->allreduce_sum(scal + kPAP, 1, st))) return rc;
@@ -731,19 +738,19 @@ struct CGRuntime {
       };
       out[0] += dt(kMFwdBeg, kMFwdEnd);
       out[1] += dt(kMStart, kMOpA);
-      out[2] += dt(kMOpA, kMBnd);
+      out[2] += dt(kMFwdEnd, kMBnd);
       out[3] += dt(kMRevBeg, kMRevEnd);
-      out[4] += dt(kMBnd, kMOpB);
-      out[5] += dt(kMOpB, kMPap);
+      out[4] += dt(kMOpA, kMJoin);
+      out[5] += dt(kMJoin, kMPap);
       out[6] += dt(kMPap, kMUpd);
       out[7] += dt(kMUpd, kMEnd);
       out[8] += dt(kMStart, kMEnd);
-      // timeline offsets from the iteration start: an exchange is hidden when
-      // it completes before the compute-stream work it overlaps does
+      // timeline offsets from the iteration start: the comm-stream chain is
+      // hidden when it completes before the interior tiles do
       out[9] += dt(kMStart, kMFwdEnd);
-      out[10] += dt(kMStart, kMOpA);
+      out[10] += dt(kMStart, kMBnd);
       out[11] += dt(kMStart, kMRevEnd);
-      out[12] += dt(kMStart, kMOpB);
+      out[12] += dt(kMStart, kMOpA);
     }
     prof = false;
     if (!rc) rc = flush();
@@ -759,7 +766,7 @@ struct CGRuntime {
     for (auto& e : pev)
       if (e) hipEventDestroy(e);
     for (hipEvent_t e : tev) hipEventDestroy(e);
-    for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_fwd, ev_bnd, ev_rev, ev_batch[0], ev_batch[1]})
+    for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_rev, ev_batch[0], ev_batch[1]})
       if (e) hipEventDestroy(e);
     if (st) hipStreamDestroy(st);
     if (cs) hipStreamDestroy(cs);
@@ -854,7 +861,7 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   if (hipStreamCreateWithFlags(&rt->st, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&rt->cs, hipStreamNonBlocking) != hipSuccess)
     return nullptr;
-  for (hipEvent_t* e : {&rt->ev_in, &rt->ev_out, &rt->ev_fork, &rt->ev_fwd, &rt->ev_bnd,
+  for (hipEvent_t* e : {&rt->ev_in, &rt->ev_out, &rt->ev_fork,
                         &rt->ev_rev, &rt->ev_batch[0], &rt->ev_batch[1]})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
   rt->face_cnt.assign(face_cnt, face_cnt + nranks);
@@ -872,11 +879,9 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   const int g1 = static_cast<int>(L.gh[1]), g2 = static_cast<int>(L.gh[2]);
   if (overlap && rt->halo && L.gh[0] == 0 && (g1 || g2)) {
     const int iy = c.nty - g1, iz = c.ntz - g2;  // interior tile extents
-    const int h = (iy + 1) / 2;
-    const int ra[4] = {0, h, 0, iz}, rb[4] = {h, iy, 0, iz};
+    const int ra[4] = {0, iy, 0, iz};
     const int r1[4] = {iy, c.nty, 0, c.ntz}, r2[4] = {0, iy, iz, c.ntz};
     std::memcpy(rt->rect_a, ra, sizeof(ra));
-    std::memcpy(rt->rect_b, rb, sizeof(rb));
     std::memcpy(rt->rect_r1, r1, sizeof(r1));
     std::memcpy(rt->rect_r2, r2, sizeof(r2));
     rt->split = true;

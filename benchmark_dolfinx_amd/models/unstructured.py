@@ -13,10 +13,10 @@ benchmark's box (the lattice is only used to *construct* the arrays); nothing
 downstream assumes a lattice, so any hexahedral mesh, cell order or dof
 numbering can be fed in (`renumbered` applies arbitrary permutations and the
 tests check the operator is equivariant under them).  `DofmapLaplacianGPU`
-runs the `lap_dofmap` HIP kernel (csrc/hip/lap_dofmap.h): the v1 sum-
-factorisation core behind the dofmap gather and an atomic scatter-add, with
-the same interior-then-boundary overlap of the forward halo exchange as the
-reference.  Vectors keep the problem's storage layout, so the halo machinery
+runs the `lap_dofmap` HIP kernel (csrc/hip/lap_dofmap.h): a wave-local
+line-per-lane sum factorisation behind the dofmap gather and an atomic
+scatter-add, with the same interior-then-boundary overlap of the forward halo
+exchange as the reference, and a fused CG iteration.  Vectors keep the problem's storage layout, so the halo machinery
 and the CG solvers are shared with the structured operators.
 """
 
@@ -114,9 +114,17 @@ class DofmapLaplacianGPU:
     geometry="otf": G per quadrature point from the cell's 8 geometry nodes;
     "stored": G precomputed once per (cell, point) in the reference layout
     [cell][6][nq^3] (src/geometry_gpu.hpp:26-132).
+
+    `apply` is the reference's operator action.  Under DeviceCG the operator
+    runs its own fused CG iteration (`cg_start` / `cg_iterate`,
+    csrc/hip/lap_dofmap.h): p = r + beta p_old, the lagged x update and the
+    p.Ap element dots ride in the gather / scatter of the operator kernel, and
+    one update pass does r -= alpha y, r.r and y = 0 -- the reference's five
+    BLAS-1 calls per iteration (src/cg.hpp:121-167) become one.
     """
 
     name = "dofmap"
+    RR0, RR1, PAP = 0, 1, 2  # DeviceCG's scalar slots
 
     def __init__(self, problem, geometry: str = "otf", mesh: UnstructuredMesh | None = None):
         if problem.platform != "gpu":
@@ -134,9 +142,14 @@ class DofmapLaplacianGPU:
             self.cverts = torch.from_numpy(m.cell_verts).to(dev)
             self.coords = torch.from_numpy(m.coords).to(dev, dt)
             self.flags = torch.from_numpy(m.dof_flags).to(dev)
+            self.tab = self.k.dofmap_tables(dev)
             self.inner = torch.from_numpy(m.interior_cells).to(dev)
             self.outer = torch.from_numpy(m.boundary_cells).to(dev)
             self.kc = None if m.kc is None else torch.from_numpy(m.kc).to(dev, dt)
+            # writer designation (sign bit of cell_dofs): the first occurrence
+            # of each dof in launch order (interior cells, then boundary cells)
+            self.k.dofmap_mark_writers(self.inner, self.outer, self.cdofs,
+                                       int(m.cell_dofs.shape[1]), m.ndofs)
             self.G = None
             self.geom = 1
             if geometry == "stored":
@@ -144,12 +157,14 @@ class DofmapLaplacianGPU:
                 self.G = torch.empty(m.ncells * 6 * nq3, dtype=dt, device=dev)
                 self.k.dofmap_geometry(m.ncells, self.cverts, self.coords, self.G)
                 self.geom = 0
+        self._cg = None
 
-    def _run(self, cells, u, y):
+    def _run(self, cells, u, y, **kw) -> int:
         n = int(cells.numel())
-        if n:
-            self.k.dofmap_apply(self.geom, cells, n, self.cdofs, self.cverts, self.coords,
-                                self.flags, self.G, self.pb.kappa, self.kc, u, y)
+        if not n:
+            return 0
+        return self.k.dofmap_apply(self.geom, self.tab, cells, n, self.cdofs, self.cverts, self.coords,
+                                   self.flags, self.G, self.pb.kappa, self.kc, u, y, **kw)
 
     def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
         pb = self.pb
@@ -159,3 +174,52 @@ class DofmapLaplacianGPU:
         pb.halo.forward_end(u, work)
         self._run(self.outer, u, y)
         pb.halo.reverse(y)
+
+    # ------------------------------------------------------------ fused CG
+    def cg_start(self, cg, x, b):
+        """r0 = b - A x0, rho0 = r0.r0 (owned), p_old = 0, y = 0."""
+        pb, k = self.pb, self.k
+        self.apply(x, cg.y)
+        k.axpy(cg.r, -1.0, cg.y, b)
+        k.dot(cg.r, cg.r, cg.partials, cg.scal, self.RR0)
+        cg._allreduce(self.RR0)
+        n = pb.lat.nstore
+        self.p_a = torch.zeros(n, dtype=pb.dtype, device=pb.device)
+        self.p_b = torch.zeros(n, dtype=pb.dtype, device=pb.device)
+        self.part = torch.zeros(int(cg.partials.numel()), dtype=torch.float64, device=pb.device)
+        cg.y.zero_()
+        self.x_lag = False
+        self._cg = cg
+
+    def cg_iterate(self, cg, n: int) -> None:
+        pb, k = self.pb, self.k
+        r, y, x, scal = cg.r.view(-1), cg.y.view(-1), cg.x.view(-1), cg.scal
+        for _ in range(n):
+            it = cg.it
+            cur, nxt = (self.RR0, self.RR1) if it % 2 == 0 else (self.RR1, self.RR0)
+            pold, pnew = (self.p_a, self.p_b) if it % 2 == 0 else (self.p_b, self.p_a)
+            kw = dict(mode=1, pold=pold, pnew=pnew, x=x, scal=scal,
+                      beta=(-1, -1) if it == 0 else (cur, nxt),
+                      xa=(nxt, self.PAP) if self.x_lag else (-1, -1))
+            work = pb.halo.forward_begin(cg.r)
+            n1 = self._run(self.inner, r, y, partials=self.part, **kw)
+            pb.halo.forward_end(cg.r, work)
+            n2 = self._run(self.outer, r, y, partials=self.part[n1:], **kw)
+            pb.halo.reverse(cg.y)
+            k.reduce_partials(self.part, n1 + n2, scal, self.PAP)
+            cg._allreduce(self.PAP)
+            nu = k.dofmap_cg_update(self.flags, r, y, scal, cur, self.PAP, self.part)
+            k.reduce_partials(self.part, nu, scal, nxt)
+            cg._allreduce(nxt)
+            self.x_lag = True
+            cg.it += 1
+        self.flush(cg)
+
+    def flush(self, cg) -> None:
+        """Apply the lagged x += alpha p of the last iteration."""
+        if not self.x_lag:
+            return
+        last = self.RR0 if (cg.it - 1) % 2 == 0 else self.RR1
+        plast = self.p_b if (cg.it - 1) % 2 == 0 else self.p_a
+        self.k.dofmap_xflush(cg.x.view(-1), plast, cg.scal, last, self.PAP)
+        self.x_lag = False

@@ -35,12 +35,12 @@ HIP_ARCH = os.environ.get("BDX_HIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def _sources(sub: str, ext: str) -> list[Path]:
-    return sorted((CSRC / sub).glob(f"*{ext}"))
+def _sources(sub: str, ext: str, csrc: Path = CSRC) -> list[Path]:
+    return sorted((csrc / sub).glob(f"*{ext}"))
 
 
-def _headers() -> list[Path]:
-    return sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "hip").glob("*.h"))
+def _headers(csrc: Path = CSRC) -> list[Path]:
+    return sorted((csrc / "include").glob("*.h")) + sorted((csrc / "hip").glob("*.h"))
 
 
 def _digest(paths: list[Path], extra: str = "") -> str:
@@ -94,26 +94,30 @@ def build_host(force: bool = False, sanitize: bool = False) -> Path:
     return out
 
 
-def hip_flags() -> list[str]:
+def hip_flags(csrc: Path = CSRC) -> list[str]:
     return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={HIP_ARCH}",
             "-munsafe-fp-atomics", "-ffp-contract=fast", "-Wno-unused-result",
-            "-I", str(CSRC / "include"), "-I", str(CSRC / "hip")]
+            "-I", str(csrc / "include"), "-I", str(csrc / "hip")]
 
 
 def build_hip(force: bool = False, jobs: int | None = None,
               extra_flags: list[str] | None = None, variant: str = "",
-              only: list[str] | None = None) -> Path:
+              only: list[str] | None = None, csrc: Path | None = None) -> Path:
     """Build libbdx_hip.so (or, with `variant`, libbdx_hip_<variant>.so with
     `extra_flags` appended: used for A/B kernel experiments on the GPU box).
     `only`: for a variant, the operator TUs (lap_fused*_*.hip stems) to keep;
-    every other operator TU is left out to save compile time."""
-    srcs = _sources("hip", ".hip")
+    every other operator TU is left out to save compile time.  `csrc`: for a
+    variant, an alternative source tree (an experimental copy of csrc/)."""
+    if csrc is None or not variant:
+        csrc = CSRC
+    csrc = Path(csrc)
+    srcs = _sources("hip", ".hip", csrc)
     if only:
         srcs = [p for p in srcs if not p.stem.startswith("lap_fused") or p.stem in only]
-    flags = hip_flags() + list(extra_flags or [])
+    flags = hip_flags(csrc) + list(extra_flags or [])
     out_so = HIP_SO if not variant else HERE / f"libbdx_hip_{variant}.so"
     obj_dir = OBJ_DIR if not variant else OBJ_DIR / variant
-    digest = _digest(srcs + _headers(), " ".join(flags))
+    digest = _digest(srcs + _headers(csrc), " ".join(flags))
     if not force and _up_to_date(out_so, digest):
         return out_so
     if not Path(HIPCC).exists():
@@ -123,7 +127,7 @@ def build_hip(force: bool = False, jobs: int | None = None,
 
     def compile_one(src: Path) -> Path:
         obj = obj_dir / (src.stem + ".o")
-        odig = _digest([src] + _headers(), " ".join(flags))
+        odig = _digest([src] + _headers(csrc), " ".join(flags))
         if not force and _up_to_date(obj, odig):
             return obj
         _run([HIPCC, *flags, "-c", str(src), "-o", str(obj)])
@@ -154,11 +158,13 @@ def main(argv=None) -> int:
                     help="also build libbdx_host_san.so (ASan + UBSan host library)")
     ap.add_argument("--only", default="",
                     help="comma-separated operator TU stems to keep in variant builds")
+    ap.add_argument("--csrc", default=None,
+                    help="variant builds: alternative source tree (a copy of csrc/)")
     a = ap.parse_args(argv)
     only = [x for x in a.only.split(",") if x] or None
     for v in a.variant:
         name, _, fl = v.partition("=")
-        print("built", build_hip(a.force, a.jobs, fl.split(), name, only))
+        print("built", build_hip(a.force, a.jobs, fl.split(), name, only, a.csrc))
     if a.variant and not (a.host or a.hip):
         return 0
     if a.sanitize:

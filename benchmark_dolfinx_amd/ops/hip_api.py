@@ -34,7 +34,10 @@ def declare(lib) -> None:
            [i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp, vp])
         _d(lib, f"bdx_geometry_{suf}", [vp, i32, vp, vp, vp, vp, vp, vp, vp])
         _d(lib, f"bdx_dofmap_apply_{suf}",
-           [i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, f64, vp, vp, vp, vp])
+           [i32, i32, i32, i32, vp, vp, i32, i64, vp, vp, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp,
+            vp, i32, i32, i32, i32, vp, vp, vp])
+        _d(lib, f"bdx_dofmap_cg_update_{suf}", [i64, vp, vp, vp, vp, i32, i32, vp, vp, vp])
+        _d(lib, f"bdx_dofmap_xflush_{suf}", [i64, vp, vp, vp, i32, i32, vp])
         _d(lib, f"bdx_dofmap_geometry_{suf}", [i32, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp])
         _d(lib, f"bdx_spmv_{suf}", [i64, vp, vp, vp, vp, vp, vp, i32, vp])
         for P in range(1, 8):
@@ -88,4 +91,5 @@ def declare(lib) -> None:
     _d(lib, "bdx_rt_destroy", [vp], None)
     _d(lib, "bdx_rt_release_group", [i64], None)
     _d(lib, "bdx_reduce_partials", [vp, i32, vp, i32, vp])
+    _d(lib, "bdx_dofmap_mark_writers", [vp, i32, vp, i32, vp, i32, vp, i64, vp])
     del ft

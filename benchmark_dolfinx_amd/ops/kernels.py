@@ -3,6 +3,8 @@ current HIP stream, errors raised loudly (no silent fallback)."""
 
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -70,13 +72,51 @@ class HipKernels:
                                        ptr(G), ptr(xv), kappa, ptr(kc), ptr(u), ptr(y), ptr(lo),
                                        ptr(hi), _stream()), "v1_apply")
 
-    def dofmap_apply(self, geom: int, cells, ncl: int, cdofs, cverts, coords, flags, G,
-                     kappa: float, kc, u, y):
+    def dofmap_tables(self, device):
+        """Device copy of the 1D tables the dofmap kernel reads as scalar loads:
+        [phi0 (nq x nd) | dphi1 (nq x nq) | qpts | wts] in the vector dtype."""
+        t = self.t
+        h = np.concatenate([t.phi0.ravel(), t.dphi1.ravel(), t.qpts.ravel(), t.wts.ravel()])
+        return torch.from_numpy(h).to(device, self.dtype)
+
+    def dofmap_apply(self, geom: int, tab, cells, ncl: int, cdofs, cverts, coords, flags, G,
+                     kappa: float, kc, u, y, mode: int = 0, pold=None, pnew=None, x=None,
+                     scal=None, beta=(-1, -1), xa=(-1, -1), partials=None) -> int:
+        """mode 0: y += A u; 1: the CG operator (u = r; see lap_dofmap.h).
+        Returns the number of p.Ap partials written (CG)."""
         t, P = self.t, self.lat.degree
-        _check(self._f("bdx_dofmap_apply")(P, t.nq, geom, ptr(t.phi0), ptr(t.dphi1), ptr(t.wts),
-                                           ptr(t.qpts), t.identity, ptr(cells), ncl, ptr(cdofs),
-                                           ptr(cverts), ptr(coords), ptr(flags), ptr(G), kappa,
-                                           ptr(kc), ptr(u), ptr(y), _stream()), "dofmap_apply")
+        nb = ctypes.c_int(0)
+        nvec = int(u.numel())
+        if nvec * u.element_size() >= 2 ** 32 - 16:
+            raise ValueError("dofmap operator: vectors beyond 4 GiB exceed the 32-bit buffer range")
+        _check(self._f("bdx_dofmap_apply")(P, t.nq, geom, mode, ptr(tab), ptr(cells), ncl, nvec,
+                                           ptr(cdofs), ptr(cverts), ptr(coords), ptr(flags),
+                                           ptr(G), kappa, ptr(kc), ptr(u), ptr(pold), ptr(pnew),
+                                           ptr(x), ptr(y), ptr(scal), beta[0], beta[1], xa[0],
+                                           xa[1], ptr(partials), ctypes.byref(nb), _stream()),
+               "dofmap_apply")
+        return nb.value
+
+    def dofmap_cg_update(self, flags, r, y, scal, rn_slot: int, pap_slot: int, partials) -> int:
+        nb = ctypes.c_int(0)
+        _check(self._f("bdx_dofmap_cg_update")(r.numel(), ptr(flags), ptr(r), ptr(y), ptr(scal),
+                                               rn_slot, pap_slot, ptr(partials), ctypes.byref(nb),
+                                               _stream()), "dofmap_cg_update")
+        return nb.value
+
+    def dofmap_xflush(self, x, p, scal, num: int, den: int):
+        _check(self._f("bdx_dofmap_xflush")(x.numel(), ptr(x), ptr(p), ptr(scal), num, den,
+                                            _stream()), "dofmap_xflush")
+
+    def dofmap_mark_writers(self, cells_a, cells_b, cdofs, nd3: int, ndofs: int):
+        first = torch.empty(max(1, ndofs), dtype=torch.int32, device=cdofs.device)
+        _check(self.lib.bdx_dofmap_mark_writers(ptr(cells_a), int(cells_a.numel()), ptr(cells_b),
+                                                int(cells_b.numel()), ptr(cdofs), nd3, ptr(first),
+                                                ndofs, _stream()), "dofmap_mark_writers")
+
+    def reduce_partials(self, partials, n: int, out, slot: int):
+        _check(self.lib.bdx_reduce_partials(ptr(partials), n, ptr(out), slot, _stream()),
+               "reduce_partials")
 
     def dofmap_geometry(self, ncells: int, cverts, coords, G):
         t, P = self.t, self.lat.degree

@@ -27,12 +27,13 @@ from ..ops.kernels import _check, _stream
 from ..ops.native import ptr
 
 
-PHASES = ("halo_fwd", "op_interior_a", "op_boundary", "halo_rev", "op_interior_b",
+PHASES = ("halo_fwd", "op_interior", "op_boundary", "halo_rev", "join_rev_add",
           "reduce_allreduce_pap", "update_rr", "allreduce_rr", "iteration",
-          # offsets from the iteration start (the exchange is hidden when its
-          # end precedes the end of the interior tiles it overlaps)
-          "t_halo_fwd_done", "t_op_interior_a_done", "t_halo_rev_done",
-          "t_op_interior_b_done")
+          # offsets from the iteration start: the comm-stream chain (forward
+          # exchange, boundary tiles, reverse send) is hidden when it ends
+          # before the interior tiles on the compute stream do
+          "t_halo_fwd_done", "t_boundary_done", "t_halo_rev_done",
+          "t_op_interior_done")
 
 
 def _agree(comm, ok: bool) -> bool:
@@ -65,11 +66,14 @@ class NativeCGRuntime:
         comm = pb.comm
         halo = pb.halo
         if use_graph is None:
-            # BDX_GRAPH=0 off, 1 (default) single rank only, 2 also with RCCL
-            # (the two-stream fork/join iteration captures RCCL calls; that
-            # has not run on a multi-GPU node yet, and the host runs far
-            # ahead of a 6 ms iteration anyway, so it is opt-in there)
-            mode = os.environ.get("BDX_GRAPH", "1")
+            # BDX_GRAPH=0 (default) eager launches at every rank count, 1 graph
+            # replay on a single rank, 2 also with RCCL (the two-stream
+            # fork/join iteration captures RCCL calls).  One launch mode for
+            # every N keeps the weak-scaling points comparable; at N = 1 graph
+            # replay and eager launches measured equal (60.12 vs 60.17 GDoF/s
+            # same box, profiles/r3_graph_ab.md): the host runs far ahead of
+            # a 5 ms iteration, so launch overhead is hidden either way.
+            mode = os.environ.get("BDX_GRAPH", "0")
             use_graph = mode == "2" or (mode == "1" and comm.size == 1)
         if overlap is None:
             overlap = os.environ.get("BDX_OVERLAP", "1") != "0"
@@ -202,8 +206,10 @@ class NativeCGRuntime:
         _check(self.lib.bdx_rt_profile(self.h, int(n), out, len(PHASES)), "rt_profile")
         self._sync_state()
         ph = {k: float(v) for k, v in zip(PHASES, out)}
-        ph["halo_fwd_hidden"] = ph["t_halo_fwd_done"] <= ph["t_op_interior_a_done"]
-        ph["halo_rev_hidden"] = ph["t_halo_rev_done"] <= ph["t_op_interior_b_done"]
+        # meaningful only for the split (two-stream) schedule
+        split = self.overlap
+        ph["halo_fwd_hidden"] = (ph["t_halo_fwd_done"] <= ph["t_op_interior_done"]) if split else None
+        ph["halo_rev_hidden"] = (ph["t_halo_rev_done"] <= ph["t_op_interior_done"]) if split else None
         return ph
 
     def close(self) -> None:

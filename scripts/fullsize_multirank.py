@@ -35,7 +35,8 @@ def main():
 
     def job(comm, dpg):
         args = bench.parse_args(["--config", a.config, "--dofs-per-gpu", str(dpg), "--steps",
-                                 str(a.steps), "--warmup", "2", "--gpus", str(comm.size)])
+                                 str(a.steps), "--warmup", "2", "--gpus", str(comm.size),
+                                 "--companions", "off", "--extras", "off"])
         out = bench.run(comm, args)
         torch.cuda.synchronize()
         return out
@@ -53,6 +54,7 @@ def main():
                           "runtime": out["config"]["runtime"],
                           "y_norm": out["config"]["y_norm"],
                           "phases_ms_max_over_ranks": out["config"]["phases_ms_max_over_ranks"],
+                          "phases_per_rank": out["config"].get("phases_per_rank"),
                           "wall_s": round(time.perf_counter() - t0, 1)}), flush=True)
     y1, yn = res[a.ref_ranks]["config"]["y_norm"], res[a.ranks]["config"]["y_norm"]
     rel = abs(y1 - yn) / abs(y1)

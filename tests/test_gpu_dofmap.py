@@ -95,12 +95,28 @@ def test_dofmap_partition_invariance_threaded(ranks):
         assert abs(xn - ref) <= 1e-11 * abs(ref), (xn, ref)
 
 
-def test_dofmap_cg_matches_host_cg():
-    gpu = PoissonProblem(Comm(), (4, 3, 5), 3, 1, False, torch.float64, "gpu", 0.1)
-    cpu = PoissonProblem(Comm(), (4, 3, 5), 3, 1, False, torch.float64, "cpu", 0.1)
+@pytest.mark.parametrize("nc,P,qm,geometry,dt,kappa", [
+    ((4, 3, 5), 3, 1, "stored", torch.float64, "constant"),
+    ((4, 3, 5), 3, 1, "otf", torch.float64, "random"),
+    ((3, 3, 4), 4, 0, "stored", torch.float64, "constant"),
+    ((2, 2, 3), 6, 1, "stored", torch.float64, "random"),
+    ((2, 2, 2), 7, 1, "otf", torch.float64, "constant"),
+    ((3, 4, 3), 3, 1, "stored", torch.float32, "constant"),
+])
+def test_dofmap_cg_matches_host_cg(nc, P, qm, geometry, dt, kappa):
+    """The fused dofmap CG iteration (p update, lagged x, p.Ap element dots
+    and the r / y update pass) against the host CG on the CPU operator."""
+    gpu = PoissonProblem(Comm(), nc, P, qm, False, dt, "gpu", 0.1, kappa)
+    cpu = PoissonProblem(Comm(), nc, P, qm, False, torch.float64, "cpu", 0.1, kappa)
     ug, uc = gpu.assemble_rhs(), cpu.assemble_rhs()
     xg, xc = gpu.new_vector(), cpu.new_vector()
-    DeviceCG(gpu).solve(DofmapLaplacianGPU(gpu, "stored"), xg, ug, 20)
+    op = DofmapLaplacianGPU(gpu, geometry)
+    cg = DeviceCG(gpu)
+    cg.start(op, xg, ug)
+    cg.iterate(7)   # two calls: the lagged x update is flushed and resumed
+    cg.iterate(13)
     torch.cuda.synchronize()
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, uc, 20, 0.0)
-    assert abs(gpu.norm(xg) - cpu.norm(xc)) <= 1e-10 * cpu.norm(xc)
+    tol = 1e-10 if dt == torch.float64 else 2e-4
+    xo, xr = cpu.owned(xg.double().cpu()), cpu.owned(xc)
+    assert (xo - xr).abs().max().item() <= tol * xr.abs().max().item()
