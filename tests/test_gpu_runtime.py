@@ -157,12 +157,16 @@ def test_phase_profile_single_and_threaded():
         op.close()
         return ph, it
     for ranks in (1, 2):
-        for ph, it in run_threaded(ranks, job):
+        res = run_threaded(ranks, job)
+        # the hidden flags exist for the split (two-stream) schedule only: a
+        # rank with ghost planes runs it, a rank without runs serially
+        if ranks > 1:
+            assert any(isinstance(ph["halo_fwd_hidden"], bool) for ph, _ in res)
+        for ph, it in res:
             assert it == 7
             assert ph["iteration"] > 0 and ph["op_interior"] > 0
             assert all(v >= 0 for v in ph.values() if isinstance(v, float))
-            # the hidden flags exist for the split (two-stream) schedule only
-            assert ranks == 1 or isinstance(ph["halo_fwd_hidden"], bool)
+            assert ph["halo_fwd_hidden"] in (True, False, None)
             for k in ("t_halo_fwd_done", "t_boundary_done", "t_halo_rev_done",
                       "t_op_interior_done"):
                 assert ph[k] <= ph["iteration"] + 1e-3, (k, ph)
