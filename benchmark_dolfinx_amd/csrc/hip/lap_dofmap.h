@@ -127,22 +127,18 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   double pap = 0.0;
 
   // 1D tables: wave-uniform scalar loads from the operator's device buffer.
-  // Each row is read through a pointer laundered with the result of the row
-  // two before it, so the loads stream with the FMAs instead of being hoisted
-  // out of the cell loop (all tables at once would overflow the SGPR file and
+  // Each contraction phase reads its table through a pointer laundered with
+  // the phase's first input value, so the phase's rows load together (one
+  // scalar-cache round trip per phase, not per row) and are not hoisted out
+  // of the cell loop (all tables at once would overflow the SGPR file and
   // spill to VGPR lanes).
   typedef const __attribute__((address_space(4))) T CT;
   constexpr int OFF_D = NQ * ND, OFF_QP = OFF_D + NQ * NQ, OFF_W = OFF_QP + NQ;
   CT* const tab0 = (CT*)A.tab;  // NOLINT: address-space cast (as in lap_fused5.h)
-  T ldep1 = T(0), ldep2 = T(0);
-  auto lrow = [&]() -> CT* {
+  auto lphase = [&](T dep) -> CT* {
     CT* p = tab0;
-    asm volatile("" : "+s"(p) : "v"(ldep2));
+    asm volatile("" : "+s"(p) : "v"(dep));
     return p;
-  };
-  auto lnext = [&](T r) {
-    ldep2 = ldep1;
-    ldep1 = r;
   };
 
   // XCD-aware bijective block remap: consecutive cell chunks on one XCD (its
@@ -340,13 +336,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
           U[rp][qx] = q_on(rp) ? Ab[(qx * NQ + qa_of(rp)) * NQP + qb_of(rp)] : T(0);
     } else {
       if (r_nod) {
+        CT* const t = lphase(ue[0]);
 #pragma unroll
         for (int qz = 0; qz < NQ; ++qz) {
-          CT* t = lrow();
           T s = T(0);
 #pragma unroll
           for (int k = 0; k < ND; ++k) s += t[qz * ND + k] * ue[k];
-          lnext(s);
           Ab[(ni * NQ + nj) * NQP + qz] = s;
         }
       }
@@ -358,13 +353,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
           T in[ND];
 #pragma unroll
           for (int j = 0; j < ND; ++j) in[j] = Ab[(mi * NQ + j) * NQP + mq];
+          CT* const t = lphase(in[0]);
 #pragma unroll
           for (int qy = 0; qy < NQ; ++qy) {
-            CT* t = lrow();
             T s = T(0);
 #pragma unroll
             for (int j = 0; j < ND; ++j) s += t[qy * ND + j] * in[j];
-            lnext(s);
             Bb[(mi * NQ + qy) * NQP + mq] = s;
           }
         }
@@ -376,13 +370,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
 #pragma unroll
         for (int i = 0; i < ND; ++i)
           in[i] = q_on(rp) ? Bb[(i * NQ + qa_of(rp)) * NQP + qb_of(rp)] : T(0);
+        CT* const t = lphase(in[0]);
 #pragma unroll
         for (int qx = 0; qx < NQ; ++qx) {
-          CT* t = lrow();
           T s = T(0);
 #pragma unroll
           for (int i = 0; i < ND; ++i) s += t[qx * ND + i] * in[i];
-          lnext(s);
           U[rp][qx] = s;
         }
         if (q_on(rp)) {
@@ -401,13 +394,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       T in[NQ], o[NQ];
 #pragma unroll
       for (int m = 0; m < NQ; ++m) in[m] = Ab[(a * NQ + m) * NQP + b];  // y-line (qx, qz)
+      CT* const t = lphase(in[0]);  // dphi1 rows for both lines
 #pragma unroll
       for (int qy = 0; qy < NQ; ++qy) {
-        CT* t = lrow();
         T s = T(0);
 #pragma unroll
         for (int m = 0; m < NQ; ++m) s += t[OFF_D + qy * NQ + m] * in[m];
-        lnext(s);
         o[qy] = s;
       }
 #pragma unroll
@@ -416,11 +408,9 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       for (int m = 0; m < NQ; ++m) in[m] = Ab[(a * NQ + b) * NQP + m];  // z-line (qx, qy)
 #pragma unroll
       for (int qz = 0; qz < NQ; ++qz) {
-        CT* t = lrow();
         T s = T(0);
 #pragma unroll
         for (int m = 0; m < NQ; ++m) s += t[OFF_D + qz * NQ + m] * in[m];
-        lnext(s);
         o[qz] = s;
       }
 #pragma unroll
@@ -439,20 +429,18 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
 #pragma unroll
       for (int rp = 0; rp < LPL; ++rp) {
         const int a = qa_of(rp), b = qb_of(rp);
+        CT* const t = lphase(U[rp][0]);
 #pragma unroll
         for (int qx = 0; qx < NQ; ++qx) {
           Fx[rp][qx] = T(0);
           if (!q_on(rp)) continue;
-          CT* t = lrow();
           T gx = T(0);
 #pragma unroll
           for (int m = 0; m < NQ; ++m) gx += t[OFF_D + qx * NQ + m] * U[rp][m];
-          lnext(gx);
           const T gy = Bb[(qx * NQ + a) * NQP + b], gz = Cb[(qx * NQ + a) * NQP + b];
           T Gd[6];
-          CT* tq = lrow();
-          geometry_G<T>(Xc, tq[OFF_QP + qx], tq[OFF_QP + a], tq[OFF_QP + b],
-                        tq[OFF_W + qx] * tq[OFF_W + a] * tq[OFF_W + b], Gd);
+          geometry_G<T>(Xc, t[OFF_QP + qx], t[OFF_QP + a], t[OFF_QP + b],
+                        t[OFF_W + qx] * t[OFF_W + a] * t[OFF_W + b], Gd);
           const T kv = valid ? kap : T(0);
           Fx[rp][qx] = kv * (Gd[0] * gx + Gd[1] * gy + Gd[2] * gz);
           Bb[(qx * NQ + a) * NQP + b] = kv * (Gd[1] * gx + Gd[3] * gy + Gd[4] * gz);
@@ -463,15 +451,14 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
 #pragma unroll
       for (int rp = 0; rp < LPL; ++rp) {
         const int a = qa_of(rp), b = qb_of(rp);
+        CT* const t = lphase(U[rp][0]);
 #pragma unroll
         for (int qx = 0; qx < NQ; ++qx) {
           Fx[rp][qx] = T(0);
           if (!q_on(rp)) continue;
-          CT* t = lrow();
           T gx = T(0);
 #pragma unroll
           for (int m = 0; m < NQ; ++m) gx += t[OFF_D + qx * NQ + m] * U[rp][m];
-          lnext(gx);
           const T gy = Bb[(qx * NQ + a) * NQP + b], gz = Cb[(qx * NQ + a) * NQP + b];
           T Gd[6];
 #pragma unroll
@@ -498,13 +485,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       T in[NQ], o[NQ];
 #pragma unroll
       for (int m = 0; m < NQ; ++m) in[m] = Bb[(a * NQ + m) * NQP + b];
+      CT* const t = lphase(in[0]);  // dphi1 columns for both lines
 #pragma unroll
       for (int qy = 0; qy < NQ; ++qy) {
-        CT* t = lrow();
         T s = T(0);
 #pragma unroll
         for (int m = 0; m < NQ; ++m) s += t[OFF_D + m * NQ + qy] * in[m];
-        lnext(s);
         o[qy] = s;
       }
 #pragma unroll
@@ -513,11 +499,9 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       for (int m = 0; m < NQ; ++m) in[m] = Cb[(a * NQ + b) * NQP + m];
 #pragma unroll
       for (int qz = 0; qz < NQ; ++qz) {
-        CT* t = lrow();
         T s = T(0);
 #pragma unroll
         for (int m = 0; m < NQ; ++m) s += t[OFF_D + m * NQ + qz] * in[m];
-        lnext(s);
         o[qz] = s;
       }
 #pragma unroll
@@ -528,13 +512,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
 #pragma unroll
     for (int rp = 0; rp < LPL; ++rp) {
       const int a = qa_of(rp), b = qb_of(rp);
+      CT* const t = lphase(Fx[rp][0]);
 #pragma unroll
       for (int qx = 0; qx < NQ; ++qx) {
-        CT* t = lrow();
         T s = q_on(rp) ? Bb[(qx * NQ + a) * NQP + b] + Cb[(qx * NQ + a) * NQP + b] : T(0);
 #pragma unroll
         for (int m = 0; m < NQ; ++m) s += t[OFF_D + m * NQ + qx] * Fx[rp][m];
-        lnext(s);
         R[rp][qx] = s;
       }
     }
@@ -559,13 +542,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
 #pragma unroll
       for (int rp = 0; rp < LPL; ++rp) {
         if (!q_on(rp)) continue;
+        CT* const t = lphase(R[rp][0]);
 #pragma unroll
         for (int i = 0; i < ND; ++i) {
-          CT* t = lrow();
           T s = T(0);
 #pragma unroll
           for (int qx = 0; qx < NQ; ++qx) s += t[qx * ND + i] * R[rp][qx];
-          lnext(s);
           Ab[(i * NQ + qa_of(rp)) * NQP + qb_of(rp)] = s;
         }
       }
@@ -577,13 +559,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
           T in[NQ];
 #pragma unroll
           for (int qy = 0; qy < NQ; ++qy) in[qy] = Ab[(mi * NQ + qy) * NQP + mq];
+          CT* const t = lphase(in[0]);
 #pragma unroll
           for (int j = 0; j < ND; ++j) {
-            CT* t = lrow();
             T s = T(0);
 #pragma unroll
             for (int qy = 0; qy < NQ; ++qy) s += t[qy * ND + j] * in[qy];
-            lnext(s);
             Bb[(mi * NQ + j) * NQP + mq] = s;
           }
         }
@@ -593,13 +574,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
         T in[NQ];
 #pragma unroll
         for (int qz = 0; qz < NQ; ++qz) in[qz] = Bb[(ni * NQ + nj) * NQP + qz];
+        CT* const t = lphase(in[0]);
 #pragma unroll
         for (int k = 0; k < ND; ++k) {
-          CT* t = lrow();
           T s = T(0);
 #pragma unroll
           for (int qz = 0; qz < NQ; ++qz) s += t[qz * ND + k] * in[qz];
-          lnext(s);
           ye[k] = s;
         }
       }
