@@ -258,11 +258,11 @@ class FusedLaplacianGPU:
                 self._rt.bind_x(x)  # DeviceCG.start may pass another iterate
                 self._rt.reset()
 
-    def cg_iterate(self, cg, n):
+    def cg_iterate(self, cg, n, flush=True):
         if self.version >= 2 and self._rt is not None:
             return self._rt.iterate(n)
         if self.version >= 2:
-            return self._cg_iterate2(cg, n)
+            return self._cg_iterate2(cg, n, flush)
         k, r, y, x, scal = cg.k, cg.r, cg.y, cg.x, cg.scal
         halo = self.pb.halo
         for _ in range(n):
@@ -280,7 +280,7 @@ class FusedLaplacianGPU:
             self.p_old, self.p_new = self.p_new, self.p_old
             cg.it += 1
 
-    def _cg_iterate2(self, cg, n):
+    def _cg_iterate2(self, cg, n, flush=True):
         """fused2 CG iteration: x += alpha_prev p_old rides in the fused
         kernel's staging (lagged one iteration, flushed at the end); the tile
         interface partials are folded inside the r update (no finalize pass
@@ -313,7 +313,8 @@ class FusedLaplacianGPU:
             self.p_old, self.p_new = self.p_new, self.p_old
             self.x_lag = True
             cg.it += 1
-        self.flush_x(cg)
+        if flush:
+            self.flush_x(cg)
 
     def flush_x(self, cg):
         """Apply the pending x += alpha_last p_last of the lagged update."""

@@ -191,7 +191,9 @@ class DofmapLaplacianGPU:
         self.x_lag = False
         self._cg = cg
 
-    def cg_iterate(self, cg, n: int) -> None:
+    def cg_iterate(self, cg, n: int, flush: bool = True) -> None:
+        """n fused CG iterations; `flush=False` leaves the last lagged x
+        update pending (a later call or `flush` applies it)."""
         pb, k = self.pb, self.k
         r, y, x, scal = cg.r.view(-1), cg.y.view(-1), cg.x.view(-1), cg.scal
         for _ in range(n):
@@ -213,7 +215,8 @@ class DofmapLaplacianGPU:
             cg._allreduce(nxt)
             self.x_lag = True
             cg.it += 1
-        self.flush(cg)
+        if flush:
+            self.flush(cg)
 
     def flush(self, cg) -> None:
         """Apply the lagged x += alpha p of the last iteration."""

@@ -81,11 +81,13 @@ class DeviceCG:
         k.dot(p, r, self.partials, scal, self.RR0)
         self._allreduce(self.RR0)
 
-    def iterate(self, n: int) -> None:
-        """Run n CG iterations (state persists across calls)."""
+    def iterate(self, n: int, flush: bool = True) -> None:
+        """Run n CG iterations (state persists across calls).  A fused
+        operator lags its x update by one iteration; `flush=False` leaves the
+        last one pending for the next call (x is then one update behind)."""
         op, x = self.op, self.x
         if hasattr(op, "cg_iterate"):
-            op.cg_iterate(self, n)
+            op.cg_iterate(self, n, flush=flush)
             return
         k, r, y, p, scal = self.k, self.r, self.y, self.p, self.scal
         for _ in range(n):
@@ -112,7 +114,9 @@ class DeviceCG:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
         ev[0].record()
         for i in range(n):
-            self.iterate(1)
+            # one x flush at the end of the timed window (inside the last
+            # step), as the native runtime's iterate(n) does
+            self.iterate(1, flush=i == n - 1)
             ev[i + 1].record()
         ev[n].synchronize()
         return [ev[i].elapsed_time(ev[i + 1]) for i in range(n)]

@@ -114,7 +114,8 @@ def test_dofmap_cg_matches_host_cg(nc, P, qm, geometry, dt, kappa):
     cg = DeviceCG(gpu)
     cg.start(op, xg, ug)
     cg.iterate(7)   # two calls: the lagged x update is flushed and resumed
-    cg.iterate(13)
+    ms = cg.iterate_timed(13)  # per-step calls, one flush at the end (bench path)
+    assert len(ms) == 13
     torch.cuda.synchronize()
     cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, uc, 20, 0.0)
     tol = 1e-10 if dt == torch.float64 else 2e-4
