@@ -61,10 +61,6 @@ def parse_args(argv=None):
     ap.add_argument("--mesh", default=None,
                     help="experiments only: explicit global cell counts NX,NY,NZ instead of "
                          "the config's DoF target")
-    ap.add_argument("--device-warmup-s", type=float, default=0.0,
-                    help="seconds of throw-away CG iterations before the warmup steps "
-                         "(a fresh device's clocks ramp up under load); the solver is "
-                         "then restarted from x = 0, so the timed steps are unchanged")
     ap.add_argument("--profile-steps", type=int, default=5,
                     help="extra eager iterations with hipEvent phase timers (0: none)")
     ap.add_argument("--companions", default="auto", choices=["auto", "on", "off"],
@@ -86,8 +82,7 @@ def _median(v):
 
 
 def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
-             kernel="auto", geometry="auto", profile_steps=0, device_warmup_s=0.0,
-             log=None) -> dict:
+             kernel="auto", geometry="auto", profile_steps=0, log=None) -> dict:
     """Build one config, run `warmup` untimed and `steps` timed CG
     iterations (barrier + device sync on both sides, MAX over ranks) and
     return its record (identical on every rank)."""
@@ -132,25 +127,8 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
             torch.cuda.synchronize()
 
     cg = None
-    dev_warm = 0
     if gpu:
         cg = DeviceCG(pb)
-        if device_warmup_s > 0:
-            # clock ramp of a fresh device: throw-away iterations, then a
-            # restart from x = 0 (the timed run is the same as without them).
-            # The count comes from the slowest rank's first batch, so every
-            # rank runs the same collectives.
-            cg.start(op, x, u)
-            tw = time.perf_counter()
-            cg.iterate(8)
-            cg.wait()
-            t8 = comm.allreduce_scalar(time.perf_counter() - tw, "max")
-            nb = min(1000, max(0, int(device_warmup_s / max(t8, 1e-6)) - 1))
-            for _ in range(nb):
-                cg.iterate(8)
-            cg.wait()
-            dev_warm = 8 * (nb + 1)
-            x.zero_()
         cg.start(op, x, u)
         cg.iterate(warmup)
         cg.wait()
@@ -178,7 +156,7 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
     if trace and comm.rank == 0:
         with open(trace, "a") as f:
             f.write(json.dumps({"config": config, "kernel": kernel, "perturb": perturb,
-                                "device_warmup_iters": dev_warm, "step_ms": step_ms}) + "\n")
+                                "step_ms": step_ms}) + "\n")
     ynorm = pb.norm(x)
     rt = getattr(op, "_rt", None)
     rec = {
@@ -188,7 +166,6 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
         "ms_per_step_min": smin,
         "steps": steps,
         "warmup": warmup,
-        "device_warmup_iters": dev_warm,
         "vs_baseline": (value / (base * n)) if base else None,
         "dtype": "fp64" if bits == 64 else "fp32",
         "degree": degree,
@@ -283,7 +260,7 @@ def run(comm, a) -> dict | None:
 
     head = _measure(comm, a, a.config, a.steps, a.warmup, kappa=a.kappa, perturb=a.perturb,
                     kernel=a.kernel, geometry=a.geometry, profile_steps=a.profile_steps,
-                    device_warmup_s=a.device_warmup_s, log=log)
+                    log=log)
     # the metric's second half: Q6 at 500 M DoFs/GPU, FP64 and FP32, on the
     # same clock discipline as the headline (own steps / warmup / ms_per_step)
     companions = {}
@@ -355,7 +332,6 @@ def run(comm, a) -> dict | None:
             "y_norm": head["y_norm"],
             "setup_s": head["setup_s"],
             "setup_phases_s": head["setup_phases_s"],
-            "device_warmup_iters": head["device_warmup_iters"],
             "device": _device_name() if gpu else "cpu",
             "build_flags": flags,
             "comm": head["comm"],
