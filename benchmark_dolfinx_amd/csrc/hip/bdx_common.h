@@ -21,6 +21,12 @@ constexpr int kFusedTabMax = 2 * 9 * 12 + 9 * 8 + 8 * 12;
 
 enum { kGeomStored = 0, kGeomOTF = 1 };
 
+// Lagged x update of the fused5 CG (Fused2Args::xmode, bits 4-5 of the apply
+// entry points' mode word, set by runtime.hip): one term per iteration, save
+// alpha_prev only, or fold two terms; the saved alpha's slot of the CG scalars.
+enum { kXSingle = 0, kXSave = 1, kXPair = 2 };
+constexpr int kScalXSave = 3;
+
 // Debug builds (BDX_DEBUG=1: `python -m benchmark_dolfinx_amd.ops.build
 // --variant debug=-DBDX_DEBUG=1`, loaded with BDX_HIP_LIB) turn on
 // device-side checks of the operator kernels' LDS and global index paths; a

@@ -184,7 +184,8 @@ template <typename T>
 __global__ void __launch_bounds__(256)
     xflush_flat_kernel(int64_t nvec, T* __restrict__ x, const T* __restrict__ p,
                        const double* __restrict__ scal, int num, int den) {
-  const T alpha = static_cast<T>(scal[num] / scal[den]);
+  // den < 0: alpha stored directly in scal[num] (kScalXSave, runtime.hip)
+  const T alpha = static_cast<T>(den < 0 ? scal[num] : scal[num] / scal[den]);
   constexpr int W = 16 / sizeof(T);
   typedef T V __attribute__((ext_vector_type(W)));
   for (int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; v < nvec;
@@ -200,7 +201,8 @@ template <typename T>
 __global__ void __launch_bounds__(256)
     xflush_kernel(int64_t L1, int64_t ld, int64_t o0, int64_t o1, int64_t o2, T* __restrict__ x,
                   const T* __restrict__ p, const double* __restrict__ scal, int num, int den) {
-  const T alpha = static_cast<T>(scal[num] / scal[den]);
+  // den < 0: alpha stored directly in scal[num] (kScalXSave, runtime.hip)
+  const T alpha = static_cast<T>(den < 0 ? scal[num] : scal[num] / scal[den]);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t nrows = o0 * o1;
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + wid; row < nrows;

@@ -55,6 +55,11 @@ struct Fused2Args {
   int nblk;                      // workgroups of the launch = rtiles * nseg
   int beta_num, beta_den;        // CG: beta = scal[num] / scal[den]; num < 0 -> 0
   int xa_num, xa_den;            // CG: alpha_prev = scal[num] / scal[den]; num < 0 -> no x update
+  // fused5 CG: paired lagged x update (kXSave, kXPair; 0 = one term per
+  // iteration).  kXSave: no x update, alpha_prev is stored to
+  // scal[kScalXSave]; kXPair: x += alpha_prev p_old + scal[kScalXSave] p_prev2,
+  // p_prev2 being read from pnew before it is overwritten (runtime.hip).
+  int xmode;
   T kappa;
   // tiled vector storage (bdx_lattice.h; tsy = 0: lattice layout): the
   // x-plane stride ps is then tsy * tsz and a node's (y, z) offset is its
@@ -790,6 +795,7 @@ int fused2_resident(int affine) {
 template <typename T>
 inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int ntz) {
   const BdxLattice L = BdxLattice::from(latd);
+  a.xmode = 0;
   const int64_t P = L.P;
   // 32-bit per-layer offsets: one layer of the vector must be < 2^31 elements
   if ((P + 1) * L.L[1] * L.ld >= (int64_t(1) << 31)) return static_cast<int>(hipErrorInvalidValue);

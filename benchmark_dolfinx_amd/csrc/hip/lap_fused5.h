@@ -170,11 +170,19 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
   T* const Wb = s_w + wv * WB;             // this wave's buffer
   T* const Wc = Wb + cw * ND2 * NDP;       // this cell's rows of array 0
 
-  T beta = T(0), xalpha = T(0);
-  const bool xupd = MODE == kFusedCG && A.xa_num >= 0;
+  // lagged x update: x += alpha_prev p_old (kXSingle), nothing but saving
+  // alpha_prev (kXSave), or two terms: + alpha_prev2 p_prev2 read from pnew
+  // before this iteration overwrites it (kXPair; saves the x read / write of
+  // every other iteration, runtime.hip)
+  T beta = T(0), xalpha = T(0), xalpha2 = T(0);
+  const bool xupd = MODE == kFusedCG && A.xa_num >= 0 && A.xmode != kXSave;
+  const bool xpair = xupd && A.xmode == kXPair;
   if constexpr (MODE == kFusedCG) {
     if (A.beta_num >= 0) beta = static_cast<T>(A.scal[A.beta_num] / A.scal[A.beta_den]);
     if (xupd) xalpha = static_cast<T>(A.scal[A.xa_num] / A.scal[A.xa_den]);
+    if (xpair) xalpha2 = static_cast<T>(A.scal[kScalXSave]);
+    if (A.xmode == kXSave && A.xa_num >= 0 && blockIdx.x == 0 && threadIdx.x == 0)
+      const_cast<double*>(A.scal)[kScalXSave] = A.scal[A.xa_num] / A.scal[A.xa_den];
   }
   double pap = 0.0;
 
@@ -200,7 +208,9 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
       v = ul[goff] + beta * po;
       if (xupd && (f & kOwnT)) {
         T* __restrict__ xl = A.x + (ul - A.u);
-        xl[goff] += xalpha * po;
+        T dx = xalpha * po;
+        if (xpair) dx += xalpha2 * pn[goff];  // p_prev2, before p_new replaces it
+        xl[goff] += dx;
       }
       if (f & kOwnT) pn[goff] = v;
     } else {
@@ -415,7 +425,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
     const T* __restrict__ un_r = A.u + lnext;
     const T* __restrict__ un_p = A.pold + lnext;
     T* __restrict__ un_x = A.x + lnext;
-    T pf_r[NPF], pf_p[NPF], pf_x[NPF];
+    const T* un_q = A.pnew + lnext;  // p_prev2 (kXPair), read before the staging store
+    T pf_r[NPF], pf_p[NPF], pf_x[NPF], pf_q[NPF];
     T pf_v[NPV];
     // next layer's cell coefficient rides with the prefetch: a load consumed
     // in the same layer would make the wave wait for the whole batch
@@ -426,12 +437,14 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
+      pf_q[k] = T(0);
       if (!last && (st_meta[k] & kValid)) {
         if (BDX_OOB(lnext + st_goff[k], A.vsize, "f5 prefetch")) continue;
         pf_r[k] = ld_stream(un_r + st_goff[k]);
         if constexpr (MODE == kFusedCG) {
           pf_p[k] = ld_stream(un_p + st_goff[k]);
           if (xupd && (st_meta[k] & kOwnT)) pf_x[k] = ld_stream(un_x + st_goff[k]);
+          if (xpair && (st_meta[k] & kOwnT)) pf_q[k] = ld_stream(un_q + st_goff[k]);
         }
       }
     }
@@ -683,7 +696,11 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
               if constexpr (MODE == kFusedCG) {
                 if (m & kOwnT) {
                   st_stream(pnl + st_goff[k], val);
-                  if (xupd) st_stream(un_x + st_goff[k], pf_x[k] + xalpha * pf_p[k]);
+                  if (xupd) {
+                    T xn = pf_x[k] + xalpha * pf_p[k];
+                    if (xpair) xn += xalpha2 * pf_q[k];
+                    st_stream(un_x + st_goff[k], xn);
+                  }
                 }
               }
               if ((m & kBcYZ) || gxx == A.bcx_hi) {
@@ -811,7 +828,8 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
     BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
-    mode &= 0xff;                                                                  \
+    a.xmode = (mode >> 4) & 3;                                                     \
+    mode &= 0xf;                                                                   \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \
     a.pnew = pnew;                                                                 \

@@ -453,9 +453,17 @@ struct CGRuntime {
   hipEvent_t pev[kNMarks] = {};
   // state
   long it = 0;
-  bool x_lag = false;
-  bool use_graph = true, graph_ok[2] = {false, false};
-  hipGraphExec_t graph[2] = {nullptr, nullptr};
+  // Lagged x update: `pend` terms alpha_j p_j are not yet in x (0, 1 or 2).
+  // One-term kernels fold alpha_prev p_old into x at every iteration (pend
+  // stays 1).  fused5 pairs them (xpair): an iteration with one term pending
+  // only saves alpha_prev (kXSave), the next folds both, reading p_prev2 from
+  // the p buffer it is about to overwrite (kXPair) -- x is read and written
+  // every other iteration, for one extra p read: 5.5 instead of 6 operator
+  // streams per iteration.
+  int pend = 0;
+  bool xpair = false;
+  bool use_graph = true, graph_ok[4] = {false, false, false, false};
+  hipGraphExec_t graph[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_batch[2] = {nullptr, nullptr};  // in-flight bound (iterate_on_stream)
   std::vector<hipEvent_t> tev;                  // per-step timing events
 
@@ -512,8 +520,16 @@ struct CGRuntime {
                                     s);
   }
 
+  // x mode of the next iteration (kXSingle with pend == 0: no x update)
+  int next_xmode() const {
+    if (pend == 0 || !xpair) return kXSingle;
+    return pend == 1 ? kXSave : kXPair;
+  }
+  void advance_pend(int xm) { pend = (pend == 0 || xm == kXPair) ? 1 : (xm == kXSave ? 2 : 1); }
+
   // One CG iteration with explicit parity / flags (stream-ordered, no sync).
-  int step(long k, bool first, bool xlag) {
+  // xm: kXSingle (pend 0: no x term; else alpha_prev p_old), kXSave, kXPair.
+  int step(long k, bool first, bool xlag, int xm) {
     const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
     T* pold = (k % 2 == 0) ? wpa : wpb;
     T* pnew = (k % 2 == 0) ? wpb : wpa;
@@ -521,7 +537,7 @@ struct CGRuntime {
     T* const x = wx;
     T* const y = wy;
     auto op = [&](const int* rect, hipStream_t s) {
-      return apply(1 | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
+      return apply(1 | (xm << 4) | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
                    pnew, x, y, yb, zb, cb, xv, kc, tabs, cfg.kappa, scal, partials,
                    first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1,
                    cfg.nty, cfg.ntz, rect, s);
@@ -595,28 +611,30 @@ struct CGRuntime {
     return 0;
   }
 
-  // Capture the steady-state iteration of a parity (it > 0, lagged x update).
-  bool capture(int parity) {
+  // Capture the steady-state iteration of a parity and x mode (it > 0,
+  // lagged x update pending); graph index = parity + 2 * (xm == kXPair).
+  bool capture(int parity, int xm) {
     hipGraph_t g = nullptr;
     if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
       (void)hipGetLastError();
       return false;
     }
-    const int rc = step(parity, false, true);
+    const int rc = step(parity, false, true, xm);
     const hipError_t e = hipStreamEndCapture(st, &g);
     if (rc || e != hipSuccess || !g) {
       if (g) hipGraphDestroy(g);
       (void)hipGetLastError();
       return false;
     }
-    const bool ok = hipGraphInstantiate(&graph[parity], g, nullptr, nullptr, 0) == hipSuccess;
+    const int gi = parity + 2 * (xm == kXPair);
+    const bool ok = hipGraphInstantiate(&graph[gi], g, nullptr, nullptr, 0) == hipSuccess;
     hipGraphDestroy(g);
     if (!ok) (void)hipGetLastError();
     return ok;
   }
 
   void drop_graphs() {
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
       if (graph[i]) hipGraphExecDestroy(graph[i]);
       graph[i] = nullptr;
       graph_ok[i] = false;
@@ -665,18 +683,20 @@ struct CGRuntime {
       for (long i = i0; i < n && i < i0 + kBatch; ++i) {
         const bool first = (it == 0);
         const int par = static_cast<int>(it % 2);
-        const bool steady = !first && x_lag && !prof;
-        if (steady && use_graph && tr->capturable() && !graph_ok[par]) {
-          graph_ok[par] = capture(par);
-          if (!graph_ok[par]) use_graph = false;  // fall back to eager launches
+        const int xm = next_xmode();
+        const int gi = par + 2 * (xm == kXPair);
+        const bool steady = !first && pend > 0 && !prof;
+        if (steady && use_graph && tr->capturable() && !graph_ok[gi]) {
+          graph_ok[gi] = capture(par, xm);
+          if (!graph_ok[gi]) use_graph = false;  // fall back to eager launches
         }
-        if (steady && use_graph && graph_ok[par]) {
-          BDX_CHECK(hipGraphLaunch(graph[par], st));
+        if (steady && use_graph && graph_ok[gi]) {
+          BDX_CHECK(hipGraphLaunch(graph[gi], st));
         } else {
-          const int rc = step(it, first, x_lag);
+          const int rc = step(it, first, pend > 0, xm);
           if (rc) return rc;
         }
-        x_lag = true;
+        advance_pend(xm);
         ++it;
         if (step_ms) BDX_CHECK(hipEventRecord(tev[i + 1], st));
       }
@@ -686,23 +706,31 @@ struct CGRuntime {
     return flush();
   }
 
+  // x += alpha_last p_last (and, with two terms pending, the saved
+  // alpha_prev p_prev, which is the last iteration's p_old)
   int flush() {
-    if (!x_lag) return 0;
+    if (pend == 0) return 0;
     const int last = ((it - 1) % 2 == 0) ? kRR0 : kRR1;
     T* plast = ((it - 1) % 2 == 0) ? wpb : wpa;  // p_new of the last iteration
-    x_lag = false;
-    int rc;
-    if (tiled) {
+    T* pprev = ((it - 1) % 2 == 0) ? wpa : wpb;  // its p_old
+    const bool two = pend == 2;
+    pend = 0;
+    auto one = [&](T* p, int num, int den) {
+      if (tiled) {
+        if constexpr (sizeof(T) == 8)
+          return bdx_xflush_tiled_f64(wlatd, wx, p, scal, num, den, st);
+        else
+          return bdx_xflush_tiled_f32(wlatd, wx, p, scal, num, den, st);
+      }
       if constexpr (sizeof(T) == 8)
-        rc = bdx_xflush_tiled_f64(wlatd, wx, plast, scal, last, kPAP, st);
+        return bdx_xflush_f64(cfg.latd, cfg.own, x, p, scal, num, den, st);
       else
-        rc = bdx_xflush_tiled_f32(wlatd, wx, plast, scal, last, kPAP, st);
-      return rc ? rc : export_x();
-    }
-    if constexpr (sizeof(T) == 8)
-      return bdx_xflush_f64(cfg.latd, cfg.own, x, plast, scal, last, kPAP, st);
-    else
-      return bdx_xflush_f32(cfg.latd, cfg.own, x, plast, scal, last, kPAP, st);
+        return bdx_xflush_f32(cfg.latd, cfg.own, x, p, scal, num, den, st);
+    };
+    int rc = one(plast, last, kPAP);
+    if (!rc && two) rc = one(pprev, kScalXSave, -1);
+    if (!rc && tiled) rc = export_x();
+    return rc;
   }
 
   // n eager iterations with timing events between the phases; out[i] = mean
@@ -725,9 +753,10 @@ struct CGRuntime {
     int rc = import_state();
     for (long i = 0; i < n && !rc; ++i) {
       const bool first = (it == 0);
-      rc = step(it, first, x_lag);
+      const int xm = next_xmode();
+      rc = step(it, first, pend > 0, xm);
       if (rc) break;
-      x_lag = true;
+      advance_pend(xm);
       ++it;
       if ((rc = static_cast<int>(hipEventRecord(ev_out, st)))) break;
       if ((rc = tr->wait(ev_out))) break;
@@ -808,6 +837,12 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   c.wts.assign(wts, wts + c.nq);
   c.qpts.assign(qpts, qpts + c.nq);
   rt->apply = apply_fn<T>(c.version, c.P);
+  // paired lagged x update (fused5 only; BDX_XPAIR=0 keeps one term per
+  // iteration, for A/B runs)
+  {
+    const char* e = std::getenv("BDX_XPAIR");
+    rt->xpair = c.version == 5 && !(e && e[0] == '0');
+  }
   if (!rt->apply || !tabs) return nullptr;
   if (c.version == 5) {
     rt->tabs = static_cast<const T*>(tabs);  // the operator's device table buffer
@@ -1024,7 +1059,7 @@ int bdx_rt_overlap(void* h) {
 int bdx_rt_reset(void* h) {
   return with_rt(h, [](auto* rt) {
     rt->it = 0;
-    rt->x_lag = false;
+    rt->pend = 0;
     rt->need_import = rt->tiled;  // the new prologue's r and x, at the next iterate
     return 0;
   });
@@ -1082,7 +1117,8 @@ int bdx_rt_profile(void* h, long n, double* out, int nout) {
 int bdx_rt_state(void* h, long* it, int* graphs) {
   return with_rt(h, [&](auto* rt) {
     *it = rt->it;
-    *graphs = rt->use_graph && (rt->graph_ok[0] || rt->graph_ok[1]);
+    *graphs = rt->use_graph &&
+              (rt->graph_ok[0] || rt->graph_ok[1] || rt->graph_ok[2] || rt->graph_ok[3]);
     return 0;
   });
 }

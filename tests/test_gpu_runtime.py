@@ -127,6 +127,44 @@ def test_fused5_operators_keep_their_own_tables_under_graph_replay(monkeypatch, 
         op.close()
 
 
+@pytest.mark.parametrize("tiled", ["1", "0"])
+@pytest.mark.parametrize("graph", ["0", "1"])
+@pytest.mark.parametrize("xpair", ["1", "0"])
+def test_fused5_paired_x_update_any_call_split(monkeypatch, xpair, graph, tiled):
+    """fused5's paired lagged x update (kXSave / kXPair in runtime.hip: x is
+    read and written every other iteration) against the host CG, for call
+    splits that leave 1 or 2 terms pending at the flush that ends each call,
+    through iterate, iterate_timed and the profiled iterations."""
+    monkeypatch.setenv("BDX_XPAIR", xpair)
+    monkeypatch.setenv("BDX_GRAPH", graph)
+    monkeypatch.setenv("BDX_TILED", tiled)
+    nc, P = (4, 5, 6), 3
+    pb = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "gpu")
+    if not fused_supported(pb, 5):
+        pytest.skip("no fused5 instance")
+    op = FusedLaplacianGPU(pb, "otf", 5)
+    cg = DeviceCG(pb)
+    x = pb.new_vector()
+    cg.start(op, x, pb.assemble_rhs())
+    assert op._rt is not None and op._rt.tiled == (tiled == "1")
+    total = 0
+    for kind, n in (("it", 1), ("it", 2), ("it", 5), ("timed", 4), ("prof", 3), ("it", 6),
+                    ("timed", 3)):
+        if kind == "it":
+            cg.iterate(n)
+        elif kind == "timed":
+            assert len(cg.iterate_timed(n)) == n
+        else:
+            op._rt.profile(n)
+        total += n
+        cg.wait()
+        cpu, xc = _host_cg(nc, P, 1, False, total)
+        rel = (cpu.owned(x.cpu()) - cpu.owned(xc)).abs().max().item() / xc.abs().max().item()
+        assert rel < 1e-10, (kind, n, total, rel)
+    assert cg.it == total
+    op.close()
+
+
 def test_devicecg_solves_twice_with_different_iterates():
     nc = (5, 6, 7)
     pb = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu")
@@ -189,6 +227,7 @@ def test_bench_entry_point_one_gpu():
     assert cfg["phases_ms"]["iteration"] > 0
     assert "gfx950" in cfg["device"]
     assert np.isfinite(cfg["y_norm"]) and cfg["y_norm"] > 0
+    assert line["ms_per_step_median"] > 0 and line["ms_per_step_min"] > 0
 
 
 def _tiled_job(comm, nc, P, nreps, version, dtype, coef, shear=0.0, pert=0.0):
