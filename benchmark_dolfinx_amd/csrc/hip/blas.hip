@@ -183,6 +183,31 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// End of a CG call on tiled storage: the lagged x terms folded into the tiled
+// iterate and the result exported to the lattice layout in one pass
+// (t += a1 p1 [+ a2 p2]; lat = t) instead of a flush pass per term plus a
+// conversion pass.  a = scal[num] / scal[den], den < 0: scal[num] itself.
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+    flush_export_kernel(VecIdx lat, VecIdx til, int64_t L0, int64_t L1v, int64_t L2,
+                        T* __restrict__ a, T* __restrict__ t, const T* __restrict__ p1,
+                        const T* __restrict__ p2, const double* __restrict__ scal, int num1,
+                        int den1, int num2, int den2) {
+  const T a1 = static_cast<T>(den1 < 0 ? scal[num1] : scal[num1] / scal[den1]);
+  const T a2 = p2 ? static_cast<T>(den2 < 0 ? scal[num2] : scal[num2] / scal[den2]) : T(0);
+  const int64_t n = L0 * L1v * L2;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n;
+       e += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t k = e % L2, r = e / L2, j = r % L1v, i = r / L1v;
+    const int64_t ti = til(i, j, k);
+    if (BDX_OOB(ti, ((L1v - 1) / til.tsy + 1) * til.tntz * til.tcol, "flush export")) continue;
+    T v = t[ti] + a1 * p1[ti];
+    if (p2) v += a2 * p2[ti];
+    t[ti] = v;
+    a[lat(i, j, k)] = v;
+  }
+}
+
 template <typename T>
 int box_copy_vi(int mode, T* vec, VecIdx vi, const int64_t* boxes, int nboxes, int64_t total,
                 T* buf, hipStream_t st) {
@@ -282,6 +307,24 @@ int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
     const int g = static_cast<int>(g64 < 65536 ? g64 : 65536);                \
     layout_convert_kernel<T><<<g, kBlock, 0, st>>>(dir, lv, tv, L.L[0], L.L[1], \
                                                    L.L[2], lat, tiled);       \
+    return static_cast<int>(hipGetLastError());                               \
+  }                                                                           \
+  /* tiled x += a1 p1 [+ a2 p2], exported to the lattice layout (p2 may be */ \
+  /* null) */                                                                 \
+  int bdx_flush_export_##SUF(const int64_t* latd_tiled, T* lat, T* tiled,     \
+                             const T* p1, const T* p2, const double* scal,    \
+                             int num1, int den1, int num2, int den2,          \
+                             hipStream_t st) {                                \
+    const BdxLattice L = BdxLattice::from(latd_tiled);                        \
+    if (!L.tsy) return static_cast<int>(hipErrorInvalidValue);                \
+    const VecIdx lv{L.L[1], L.ld, 0, 0, 0, 0};                                \
+    const VecIdx tv{L.L[1], L.ld, L.tsy, L.tsz, L.tntz, L.tcol};              \
+    const int64_t n = L.L[0] * L.L[1] * L.L[2];                               \
+    const int64_t g64 = (n + kBlock - 1) / kBlock;                            \
+    const int g = static_cast<int>(g64 < 65536 ? g64 : 65536);                \
+    flush_export_kernel<T><<<g, kBlock, 0, st>>>(lv, tv, L.L[0], L.L[1], L.L[2], \
+                                                 lat, tiled, p1, p2, scal, num1, \
+                                                 den1, num2, den2);           \
     return static_cast<int>(hipGetLastError());                               \
   }
 

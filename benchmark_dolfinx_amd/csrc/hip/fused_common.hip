@@ -178,24 +178,6 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
-// x += (s[num] / s[den]) p over a whole flat vector (the tiled storage: its
-// padding is zero in p, so it stays zero in x).
-template <typename T>
-__global__ void __launch_bounds__(256)
-    xflush_flat_kernel(int64_t nvec, T* __restrict__ x, const T* __restrict__ p,
-                       const double* __restrict__ scal, int num, int den) {
-  // den < 0: alpha stored directly in scal[num] (kScalXSave, runtime.hip)
-  const T alpha = static_cast<T>(den < 0 ? scal[num] : scal[num] / scal[den]);
-  constexpr int W = 16 / sizeof(T);
-  typedef T V __attribute__((ext_vector_type(W)));
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * 256) {
-    V xv = reinterpret_cast<V*>(x)[v];
-    xv += alpha * reinterpret_cast<const V*>(p)[v];
-    reinterpret_cast<V*>(x)[v] = xv;
-  }
-}
-
 // x += (s[num] / s[den]) p over the owned rows (flush of the lagged x update).
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -304,21 +286,11 @@ BDX_CGI(float, f32)
       reduce_partials_fixed<<<1, 256, 0, st>>>(partials, g, scal, out_slot);                   \
     }                                                                                          \
     return static_cast<int>(hipGetLastError());                                                \
-  }                                                                                            \
-  int bdx_xflush_tiled_##SUF(const int64_t* latd, T* x, const T* p, const double* scal, int num, \
-                             int den, hipStream_t st) {                                        \
-    const BdxLattice L = BdxLattice::from(latd);                                               \
-    const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
-    const int64_t want = (nvec + 255) / 256;                                                   \
-    const int g = static_cast<int>(want < 65536 ? (want > 0 ? want : 1) : 65536);              \
-    xflush_flat_kernel<T><<<g, 256, 0, st>>>(nvec, x, p, scal, num, den);                      \
-    return static_cast<int>(hipGetLastError());                                                \
   }
 BDX_CGT(double, f64)
 BDX_CGT(float, f32)
 #undef BDX_CGT
 
-// Timing-only phase drops compiled into this TU (0 in a valid build).
 // Tile shape (cells in y, z) used by the fused kernel for a given nq.
 int bdx_fused_tile(int nq, int* ty, int* tz) {
   switch (nq) {

@@ -412,14 +412,16 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
 
     // ------------------------------------------------ front y
     // lanes (c, qy = a, qz = b): tBB = B_y B_z u, tDB = Dd_y B_z u, tBD = B_y Dd_z u
+    // PEEL: each contraction's first term initialises its accumulators (no
+    // zeroing moves before the rolled loops): x-trilinear Q3 26.1 -> 27.3
+    // GDoF/s, Q6 neutral (scripts/r3_flushx.sh); the general instance would
+    // spill (61 VGPRs), so it keeps the zeroed accumulators.
+    constexpr bool PEEL = AFF != 0;
     T tBB[ND], tDB[ND], tBD[ND];
-#pragma unroll
-    for (int i = 0; i < ND; ++i) tBB[i] = tDB[i] = tBD[i] = T(0);
     {
       const T* __restrict__ bra = s_tab + OFF_BR + a * NP;
       const T* __restrict__ dra = s_tab + OFF_DR + a * NP;
-BDX_PRAGMA_UNROLL(2)
-      for (int j = 0; j < ND; ++j) {
+      auto row = [&](int j, bool first) __attribute__((always_inline)) {
         T rb[ND], rd[ND];
         const int o = offA(c, j, b);
         ldrow<ND>(W0 + o, rb);
@@ -427,11 +429,19 @@ BDX_PRAGMA_UNROLL(2)
         const T cb_ = bra[j], cd_ = dra[j];
 #pragma unroll
         for (int i = 0; i < ND; ++i) {
-          tBB[i] += cb_ * rb[i];
-          tDB[i] += cd_ * rb[i];
-          tBD[i] += cb_ * rd[i];
+          tBB[i] = first ? cb_ * rb[i] : tBB[i] + cb_ * rb[i];
+          tDB[i] = first ? cd_ * rb[i] : tDB[i] + cd_ * rb[i];
+          tBD[i] = first ? cb_ * rd[i] : tBD[i] + cb_ * rd[i];
         }
+      };
+      if constexpr (PEEL) {
+        row(0, true);
+      } else {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) tBB[i] = tDB[i] = tBD[i] = T(0);
       }
+BDX_PRAGMA_UNROLL((PEEL ? 3 : 2))
+      for (int j = PEEL ? 1 : 0; j < ND; ++j) row(j, false);
     }
 
     // ------------------------------------------------ geometry coefficients
@@ -519,10 +529,7 @@ BDX_PRAGMA_UNROLL(2)
     //   g = (Dd_x tBB, B_x tDB, B_x tBD)(q),  F = kappa G g,
     //   a1 += Dd_x^T Fx, a2 += B_x^T Fy, a3 += B_x^T Fz
     T a1[ND], a2[ND], a3[ND];
-#pragma unroll
-    for (int i = 0; i < ND; ++i) a1[i] = a2[i] = a3[i] = T(0);
-BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
-    for (int q = 0; q < NQ; ++q) {
+    auto xpoint = [&](int q, bool first) __attribute__((always_inline)) {
       T gxq = 0, gyq = 0, gzq = 0;
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
@@ -570,11 +577,19 @@ BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
         const T dq = gt[OFF_DC + i * XP + q], bq = gt[OFF_BC + i * XP + q];
-        a1[i] += dq * fx;
-        a2[i] += bq * fy;
-        a3[i] += bq * fz;
+        a1[i] = first ? dq * fx : a1[i] + dq * fx;
+        a2[i] = first ? bq * fy : a2[i] + bq * fy;
+        a3[i] = first ? bq * fz : a3[i] + bq * fz;
       }
+    };
+    if constexpr (PEEL) {
+      xpoint(0, true);
+    } else {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) a1[i] = a2[i] = a3[i] = T(0);
     }
+BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
+    for (int q = PEEL ? 1 : 0; q < NQ; ++q) xpoint(q, false);
     if constexpr (WAVELOCAL) {
       // W0 <- A1, W1 <- A2 (the front-y reads of this wave are already issued)
       wave_order();
@@ -634,13 +649,10 @@ BDX_PRAGMA_UNROLL(2)
       cell_sync();
       // back y: lanes (c, j = a < ND, qz = b): C1 = B_y^T A1 + Dd_y^T A2, C3 = B_y^T A3
       T c1[ND], c3[ND];
-#pragma unroll
-      for (int i = 0; i < ND; ++i) c1[i] = c3[i] = T(0);
       if (lane_on && a < ND) {
         const T* bcj = s_tab + OFF_BC + a * XP;
         const T* dcj = s_tab + OFF_DC + a * XP;
-BDX_PRAGMA_UNROLL(2)
-        for (int qy = 0; qy < NQ; ++qy) {
+        auto row = [&](int qy, bool first) __attribute__((always_inline)) {
           const int o = offA(c, qy, b);
           T r1[ND], r2[ND], r3[ND];
           ldrow<ND>(W0 + o, r1);
@@ -649,10 +661,21 @@ BDX_PRAGMA_UNROLL(2)
           const T bq = bcj[qy], dq = dcj[qy];
 #pragma unroll
           for (int i = 0; i < ND; ++i) {
-            c1[i] += bq * r1[i] + dq * r2[i];
-            c3[i] += bq * r3[i];
+            c1[i] = first ? bq * r1[i] + dq * r2[i] : c1[i] + bq * r1[i] + dq * r2[i];
+            c3[i] = first ? bq * r3[i] : c3[i] + bq * r3[i];
           }
+        };
+        if constexpr (PEEL) {
+          row(0, true);
+        } else {
+#pragma unroll
+          for (int i = 0; i < ND; ++i) c1[i] = c3[i] = T(0);
         }
+BDX_PRAGMA_UNROLL(2)
+        for (int qy = PEEL ? 1 : 0; qy < NQ; ++qy) row(qy, false);
+      } else {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) c1[i] = c3[i] = T(0);
       }
       cell_sync();  // every wave's back-y reads done before C overwrites A1/A2
       if (lane_on && a < ND) {
@@ -665,21 +688,30 @@ BDX_PRAGMA_UNROLL(2)
     // ------------------------------------------------ back z
     // lanes (c, j = a < ND, k = b < ND): y_e = B_z^T C1 + Dd_z^T C3
     T ye[ND];
-#pragma unroll
-    for (int i = 0; i < ND; ++i) ye[i] = T(0);
     if (lane_on && a < ND && b < ND) {
       const T* bck = s_tab + OFF_BC + b * XP;
       const T* dck = s_tab + OFF_DC + b * XP;
-BDX_PRAGMA_UNROLL(2)
-      for (int qz = 0; qz < NQ; ++qz) {
+      auto row = [&](int qz, bool first) __attribute__((always_inline)) {
         const int o = offA(c, a, qz);
         T r1[ND], r3[ND];
         ldrow<ND>(W0 + o, r1);
         ldrow<ND>(W1 + o, r3);
         const T bq = bck[qz], dq = dck[qz];
 #pragma unroll
-        for (int i = 0; i < ND; ++i) ye[i] += bq * r1[i] + dq * r3[i];
+        for (int i = 0; i < ND; ++i)
+          ye[i] = first ? bq * r1[i] + dq * r3[i] : ye[i] + bq * r1[i] + dq * r3[i];
+      };
+      if constexpr (PEEL) {
+        row(0, true);
+      } else {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) ye[i] = T(0);
       }
+BDX_PRAGMA_UNROLL(2)
+      for (int qz = PEEL ? 1 : 0; qz < NQ; ++qz) row(qz, false);
+    } else {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) ye[i] = T(0);
     }
 
     // ------------------------------------------------ element vectors -> A1 of the cell

@@ -79,16 +79,16 @@ int bdx_box_copy_lat_f32(int, float*, const int64_t*, const int64_t*, int, int64
                          hipStream_t);
 int bdx_layout_convert_f64(int, const int64_t*, double*, double*, hipStream_t);
 int bdx_layout_convert_f32(int, const int64_t*, float*, float*, hipStream_t);
+int bdx_flush_export_f64(const int64_t*, double*, double*, const double*, const double*,
+                         const double*, int, int, int, int, hipStream_t);
+int bdx_flush_export_f32(const int64_t*, float*, float*, const float*, const float*,
+                         const double*, int, int, int, int, hipStream_t);
 int bdx_cg_update_tiled_f64(const int64_t*, const int64_t*, double*, const double*, const double*,
                             const double*, const double*, int, int, double*, int, int, int,
                             double*, hipStream_t);
 int bdx_cg_update_tiled_f32(const int64_t*, const int64_t*, float*, const float*, const float*,
                             const float*, const float*, int, int, double*, int, int, int, double*,
                             hipStream_t);
-int bdx_xflush_tiled_f64(const int64_t*, double*, const double*, const double*, int, int,
-                         hipStream_t);
-int bdx_xflush_tiled_f32(const int64_t*, float*, const float*, const double*, int, int,
-                         hipStream_t);
 }
 
 // The fused2..5 operator entry points (lap_fused{2,3,4,5}_<suf>_p<P>.hip);
@@ -492,7 +492,6 @@ struct CGRuntime {
     const BdxLattice L = BdxLattice::from(cfg.latdT);
     return static_cast<int>(hipMemsetAsync(pat, 0, L.size() * sizeof(T), st));
   }
-  int export_x() { return tiled ? convert(1, x, xt, st) : 0; }
   // forward: owned lower faces of v -> peers' ghost planes (pack, exchange, unpack)
   int halo_forward(T* v, hipStream_t s) {
     int rc = box_copy(0, v, face_boxes, nface_boxes, face_total, hbuf_a, s);
@@ -715,13 +714,16 @@ struct CGRuntime {
     T* pprev = ((it - 1) % 2 == 0) ? wpa : wpb;  // its p_old
     const bool two = pend == 2;
     pend = 0;
+    if (tiled) {  // fold the terms and export x in one pass
+      const T* p2 = two ? pprev : nullptr;
+      if constexpr (sizeof(T) == 8)
+        return bdx_flush_export_f64(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
+                                    -1, st);
+      else
+        return bdx_flush_export_f32(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
+                                    -1, st);
+    }
     auto one = [&](T* p, int num, int den) {
-      if (tiled) {
-        if constexpr (sizeof(T) == 8)
-          return bdx_xflush_tiled_f64(wlatd, wx, p, scal, num, den, st);
-        else
-          return bdx_xflush_tiled_f32(wlatd, wx, p, scal, num, den, st);
-      }
       if constexpr (sizeof(T) == 8)
         return bdx_xflush_f64(cfg.latd, cfg.own, x, p, scal, num, den, st);
       else
@@ -729,7 +731,6 @@ struct CGRuntime {
     };
     int rc = one(plast, last, kPAP);
     if (!rc && two) rc = one(pprev, kScalXSave, -1);
-    if (!rc && tiled) rc = export_x();
     return rc;
   }
 
