@@ -585,6 +585,22 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       }
     }
 
+    // ---- element dot p_e . (A_e p_e); the element vector and its dof ids
+    // (-1: Dirichlet / no cell) go to LDS in local-dof order for the scatter
+    dof_wave_sync();  // every lane has read the last stage's buffer
+    int* const Di = reinterpret_cast<int*>(Ab);
+    if (r_nod) {
+#pragma unroll
+      for (int k = 0; k < ND; ++k) {
+        const bool add = valid && !(fl[k] & 1u);
+        if constexpr (MODE == kDofCG) {
+          if (add) pap += static_cast<double>(ue[k]) * static_cast<double>(ye[k]);
+        }
+        Cb[(ni * ND + nj) * ND + k] = ye[k];
+        Di[(ni * ND + nj) * ND + k] = add ? (dof[k] & 0x7fffffff) : -1;
+      }
+    }
+
     // ---- advance the pipeline: the next cell's gathers and G, the dofs of
     // the one after (issued before this cell's atomics, which need no wait)
     {
@@ -597,14 +613,22 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       cell_cur = cn;
     }
 
-    // ---- scatter-add (non-Dirichlet dofs) and the element dot p_e . (A_e p_e)
-    if (r_nod && valid) {
+    // ---- scatter-add of the non-Dirichlet dofs, one wave-instruction per 64
+    // local dofs of a cell: consecutive lanes add to consecutive local dofs
+    // (k fastest), so on a mesh whose z-lines are numbered contiguously an
+    // instruction carries ND-dof runs instead of one dof per lane (float
+    // atomics execute as 64-B memory-side requests: MI355X_MICROARCH.md,
+    // "Global float atomics")
 #pragma unroll
-      for (int k = 0; k < ND; ++k) {
-        if (fl[k] & 1u) continue;
-        const int d = dof[k] & 0x7fffffff;
-        atomicAdd(A.y + d, ye[k]);
-        if constexpr (MODE == kDofCG) pap += static_cast<double>(ue[k]) * static_cast<double>(ye[k]);
+    for (int s = 0; s < CPW; ++s) {
+      const T* const Cs = s_buf[wv][s][2];
+      const int* const Ds = reinterpret_cast<const int*>(s_buf[wv][s][0]);
+#pragma unroll
+      for (int e0 = 0; e0 < ND3; e0 += 64) {
+        if (e0 + lane < ND3) {
+          const int d = Ds[e0 + lane];
+          if (d >= 0) atomicAdd(A.y + d, Cs[e0 + lane]);
+        }
       }
     }
     dof_wave_sync();  // the next cell reuses the wave's buffers
