@@ -190,6 +190,7 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   constexpr int STEP = S::WAVES * CPW;
   constexpr int IB = 64 / CPW;               // iterations per id block
   constexpr int XPL = (24 + NQ2 - 1) / NQ2;  // vertex coordinates per lane (OTF)
+  constexpr int NE = CPW * ND3, RE = (NE + 63) / 64;  // gathered elements / rounds per lane
   const int first = c_beg + wv * CPW + slot;
   const int last_li = c_end - 1;
   const int wbase = c_beg + wv * CPW;  // list index of (iteration 0, slot 0)
@@ -201,12 +202,23 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   auto id_put = [&](int blk, int v) {
     if (lane < IB * CPW) s_ids[wv][blk & 1][lane] = v;
   };
-  auto cell_of = [&](int j) -> int { return s_ids[wv][(j / IB) & 1][(j % IB) * CPW + (slot_on ? slot : 0)]; };
-  const int nodoff = r_nod ? (ni * ND + nj) * ND : 0;
-  auto load_dofs = [&](int c32, int (&d)[ND]) {
-    const int64_t c = c32;
+  auto cell_at = [&](int j, int s) -> int { return s_ids[wv][(j / IB) & 1][(j % IB) * CPW + s]; };
+  auto cell_of = [&](int j) -> int { return cell_at(j, slot_on ? slot : 0); };
+  // element role of the gather / CG stores / scatter: lane + 64 r is entry
+  // e_ of cell slot s_ (local dofs in cell_dofs order, k fastest), so each
+  // wave-instruction reads a cell's dofmap row and its dofs' values in
+  // contiguous z-runs instead of one dof per lane
+  auto e_slot = [&](int r) { return (lane + 64 * r) / ND3; };
+  auto e_loc = [&](int r) { return (lane + 64 * r) % ND3; };
+  auto e_on = [&](int j, int r) {  // element of a cell of this launch
+    return lane + 64 * r < NE && wbase + e_slot(r) + j * STEP < c_end;
+  };
+  auto load_dofs = [&](int j, int (&d)[RE]) {
 #pragma unroll
-    for (int k = 0; k < ND; ++k) d[k] = A.cdofs[c * ND3 + nodoff + k];
+    for (int r = 0; r < RE; ++r) {
+      const int s = lane + 64 * r < NE ? e_slot(r) : 0;
+      d[r] = A.cdofs[static_cast<int64_t>(cell_at(j, s)) * ND3 + e_loc(r)];
+    }
   };
   auto load_verts = [&](int c32, int (&vx)[XPL]) {
     const int64_t c = c32;
@@ -217,20 +229,20 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     }
   };
   struct Gather {
-    T u[ND], po[ND], x[ND], X[XPL];
-    unsigned f[ND];
+    T u[RE], po[RE], x[RE], X[XPL];
+    unsigned f[RE];
     T kc;
   };
-  auto gather = [&](const int (&d)[ND], const int (&vx)[XPL], int c32, bool ok, Gather& g) {
+  auto gather = [&](const int (&d)[RE], const int (&vx)[XPL], int j, int c32, Gather& g) {
 #pragma unroll
-    for (int k = 0; k < ND; ++k) {
-      const unsigned dd = static_cast<unsigned>(d[k] & 0x7fffffff);
-      const bool on = ok & r_nod;
-      g.f[k] = __builtin_amdgcn_raw_buffer_load_b8(rs_f, on ? dd : kOOB, 0, 0);
-      g.u[k] = ldv(rs_u, on ? dd * sizeof(T) : kOOB);
-      g.po[k] = MODE == kDofCG ? ldv(rs_po, on ? dd * sizeof(T) : kOOB) : T(0);
-      const bool xw = on & (d[k] < 0) & (MODE == kDofCG) & (A.xa_num >= 0);
-      g.x[k] = MODE == kDofCG ? ldv(rs_x, xw ? dd * sizeof(T) : kOOB) : T(0);
+    for (int r = 0; r < RE; ++r) {
+      const unsigned dd = static_cast<unsigned>(d[r] & 0x7fffffff);
+      const bool on = e_on(j, r);
+      g.f[r] = __builtin_amdgcn_raw_buffer_load_b8(rs_f, on ? dd : kOOB, 0, 0);
+      g.u[r] = ldv(rs_u, on ? dd * sizeof(T) : kOOB);
+      g.po[r] = MODE == kDofCG ? ldv(rs_po, on ? dd * sizeof(T) : kOOB) : T(0);
+      const bool xw = on & (d[r] < 0) & (MODE == kDofCG) & (A.xa_num >= 0);
+      g.x[r] = MODE == kDofCG ? ldv(rs_x, xw ? dd * sizeof(T) : kOOB) : T(0);
     }
 #pragma unroll
     for (int e = 0; e < XPL; ++e) {
@@ -256,25 +268,25 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
 
   const bool wave_on = wbase < c_end;
   const int nit = wave_on ? (c_end - wbase + STEP - 1) / STEP : 0;  // iterations of this wave
-  int dA[ND], dB[ND], vA[XPL], vB[XPL];
+  int dA[RE], dB[RE], vA[XPL], vB[XPL];
   int cell_cur = 0, id_next = 0;
   Gather gc;
   if (wave_on) {
     id_put(0, id_load(0));
     dof_wave_sync();
     cell_cur = cell_of(0);
-    load_dofs(cell_cur, dA);
+    load_dofs(0, dA);
     load_verts(cell_cur, vA);
-    gather(dA, vA, cell_cur, slot_on && first < c_end, gc);
+    gather(dA, vA, 0, cell_cur, gc);
     load_G(cell_cur);
-    load_dofs(cell_of(1), dB);
+    load_dofs(1, dB);
     load_verts(cell_of(1), vB);
   }
 
   // one cell of the pipeline: (dc, vc) hold its dofs / vertices (landed),
   // (dn, vn) the next cell's (in flight); the advance overwrites (dc, vc)
   // with the dofs of the cell after next
-  auto iter = [&](int j, int (&dc)[ND], int (&dn)[ND], int (&vc)[XPL], int (&vn)[XPL])
+  auto iter = [&](int j, int (&dc)[RE], int (&dn)[RE], int (&vc)[XPL], int (&vn)[XPL])
       __attribute__((always_inline)) {
     const int li = first + j * STEP;
     const bool valid = slot_on && li < c_end;
@@ -286,32 +298,38 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     if (j % IB == IB / 2) id_put(j / IB + 1, id_next);
     const T kap = A.kc ? gc.kc : A.kappa;
 
-    // ---- the gathered z-line of lane (i, j): p = r + beta p_old (CG), the
-    // writer's p / lagged x stores, Dirichlet identity rows
-    int dof[ND];
-    unsigned fl[ND];
-    T ue[ND];
+    // ---- the gathered elements (element role): p = r + beta p_old (CG), the
+    // writer's p / lagged x stores, Dirichlet identity rows; the element
+    // vector goes to LDS in the nodal layout, the scatter target stays here
+    // (-1: Dirichlet dof, entry of no cell)
+    int dsc[RE];
+    T ue[RE];
 #pragma unroll
-    for (int k = 0; k < ND; ++k) {
-      dof[k] = dc[k];
-      const int d = dof[k] & 0x7fffffff;
-      const bool on = valid && r_nod;
-      const bool wr = on && dof[k] < 0;
-      fl[k] = (on ? gc.f[k] : 0u) | (wr ? 4u : 0u);
-      T v = gc.u[k];
+    for (int r = 0; r < RE; ++r) {
+      const int dof = dc[r];
+      const int d = dof & 0x7fffffff;
+      const bool on = e_on(j, r);
+      const bool wr = on && dof < 0;
+      const unsigned fl = (on ? gc.f[r] : 0u) | (wr ? 4u : 0u);
+      T v = gc.u[r];
       if constexpr (MODE == kDofCG) {
-        v = gc.u[k] + beta * gc.po[k];
+        v = gc.u[r] + beta * gc.po[r];
         stv(rs_pn, wr ? static_cast<unsigned>(d) * sizeof(T) : kOOB, v);
         stv(rs_x, (wr && A.xa_num >= 0) ? static_cast<unsigned>(d) * sizeof(T) : kOOB,
-            gc.x[k] + xalpha * gc.po[k]);
+            gc.x[r] + xalpha * gc.po[r]);
       }
-      const bool bc = fl[k] & 1u;
-      const bool idrow = (fl[k] & 7u) == 7u;  // Dirichlet, owned, writer
+      const bool bc = fl & 1u;
+      const bool idrow = (fl & 7u) == 7u;  // Dirichlet, owned, writer
       stv(rs_y, idrow ? static_cast<unsigned>(d) * sizeof(T) : kOOB, v);
       if constexpr (MODE == kDofCG) {
         if (idrow) pap += static_cast<double>(v) * static_cast<double>(v);
       }
-      ue[k] = bc ? T(0) : v;  // zero column
+      ue[r] = bc ? T(0) : v;  // zero column
+      dsc[r] = (on && !bc) ? d : -1;
+      if (lane + 64 * r < NE) {
+        const int e = e_loc(r);
+        s_buf[wv][e_slot(r)][0][((e / (ND * ND)) * NQ + (e / ND) % ND) * NQP + e % ND] = ue[r];
+      }
     }
     if constexpr (GEOM == kGeomOTF) {
 #pragma unroll
@@ -320,28 +338,27 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
         if (slot_on && x < 24) s_X[wv][slot][x] = gc.X[e];
       }
     }
+    dof_wave_sync();
 
     // ---- interpolation to the quadrature points: z (nodal lanes), y (mixed), x (quad)
     T U[LPL][NQ];
     if constexpr (IDENT) {
-      if (r_nod) {
-#pragma unroll
-        for (int k = 0; k < ND; ++k) Ab[(ni * NQ + nj) * NQP + k] = ue[k];
-      }
-      dof_wave_sync();
 #pragma unroll
       for (int rp = 0; rp < LPL; ++rp)
 #pragma unroll
         for (int qx = 0; qx < NQ; ++qx)
           U[rp][qx] = q_on(rp) ? Ab[(qx * NQ + qa_of(rp)) * NQP + qb_of(rp)] : T(0);
     } else {
-      if (r_nod) {
-        CT* const t = lphase(ue[0]);
+      if (r_nod) {  // z-line (i, j) of the element vector, rewritten in place
+        T un[ND];
+#pragma unroll
+        for (int k = 0; k < ND; ++k) un[k] = Ab[(ni * NQ + nj) * NQP + k];
+        CT* const t = lphase(un[0]);
 #pragma unroll
         for (int qz = 0; qz < NQ; ++qz) {
           T s = T(0);
 #pragma unroll
-          for (int k = 0; k < ND; ++k) s += t[qz * ND + k] * ue[k];
+          for (int k = 0; k < ND; ++k) s += t[qz * ND + k] * un[k];
           Ab[(ni * NQ + nj) * NQP + qz] = s;
         }
       }
@@ -585,20 +602,11 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       }
     }
 
-    // ---- element dot p_e . (A_e p_e); the element vector and its dof ids
-    // (-1: Dirichlet / no cell) go to LDS in local-dof order for the scatter
+    // ---- A_e p_e of every cell to LDS in local-dof order (k fastest)
     dof_wave_sync();  // every lane has read the last stage's buffer
-    int* const Di = reinterpret_cast<int*>(Ab);
     if (r_nod) {
 #pragma unroll
-      for (int k = 0; k < ND; ++k) {
-        const bool add = valid && !(fl[k] & 1u);
-        if constexpr (MODE == kDofCG) {
-          if (add) pap += static_cast<double>(ue[k]) * static_cast<double>(ye[k]);
-        }
-        Cb[(ni * ND + nj) * ND + k] = ye[k];
-        Di[(ni * ND + nj) * ND + k] = add ? (dof[k] & 0x7fffffff) : -1;
-      }
+      for (int k = 0; k < ND; ++k) Cb[(ni * ND + nj) * ND + k] = ye[k];
     }
 
     // ---- advance the pipeline: the next cell's gathers and G, the dofs of
@@ -606,29 +614,25 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     {
       dof_wave_sync();  // the id ring entry of j + 1 / j + 2 is visible
       const int cn = cell_of(j + 1), cnn = cell_of(j + 2);
-      gather(dn, vn, cn, slot_on && li + STEP < c_end, gc);
+      gather(dn, vn, j + 1, cn, gc);
       load_G(cn);
-      load_dofs(cnn, dc);
+      load_dofs(j + 2, dc);
       load_verts(cnn, vc);
       cell_cur = cn;
     }
 
-    // ---- scatter-add of the non-Dirichlet dofs, one wave-instruction per 64
-    // local dofs of a cell: consecutive lanes add to consecutive local dofs
-    // (k fastest), so on a mesh whose z-lines are numbered contiguously an
-    // instruction carries ND-dof runs instead of one dof per lane (float
+    // ---- element role: the element dot p_e . (A_e p_e) and the scatter-add
+    // of the non-Dirichlet dofs; consecutive lanes add to consecutive local
+    // dofs, so on a mesh whose z-lines are numbered contiguously a
+    // wave-instruction carries ND-dof runs instead of one dof per lane (float
     // atomics execute as 64-B memory-side requests: MI355X_MICROARCH.md,
     // "Global float atomics")
 #pragma unroll
-    for (int s = 0; s < CPW; ++s) {
-      const T* const Cs = s_buf[wv][s][2];
-      const int* const Ds = reinterpret_cast<const int*>(s_buf[wv][s][0]);
-#pragma unroll
-      for (int e0 = 0; e0 < ND3; e0 += 64) {
-        if (e0 + lane < ND3) {
-          const int d = Ds[e0 + lane];
-          if (d >= 0) atomicAdd(A.y + d, Cs[e0 + lane]);
-        }
+    for (int r = 0; r < RE; ++r) {
+      if (lane + 64 * r < NE && dsc[r] >= 0) {
+        const T v = s_buf[wv][e_slot(r)][2][e_loc(r)];
+        if constexpr (MODE == kDofCG) pap += static_cast<double>(ue[r]) * static_cast<double>(v);
+        atomicAdd(A.y + dsc[r], v);
       }
     }
     dof_wave_sync();  // the next cell reuses the wave's buffers
