@@ -22,7 +22,11 @@
 // src/laplacian_gpu.hpp:172-412).  Here a lane owns a whole 1D line of the
 // cell and contracts it in registers; LDS only transposes between the line
 // directions, inside the wave:
-//   nodal      lane (i, j):   z-line of the element vector (gather, scatter)
+//   element    lane + 64 r:   one local dof of one of the wave's cells, in
+//                             cell_dofs order (gather, CG stores, scatter):
+//                             a wave-instruction reads one dofmap row and
+//                             touches the dofs in z-runs, not one per lane
+//   nodal      lane (i, j):   z-line of the element vector
 //   mixed      lane (i, qz):  y-lines of the half-interpolated arrays
 //   quadrature lane (qy, qz): x-lines of U, grad U, G grad U (G loads are
 //                             contiguous across these lanes), with the y- and
