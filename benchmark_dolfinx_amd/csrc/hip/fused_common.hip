@@ -113,8 +113,13 @@ __global__ void __launch_bounds__(256)
 // arithmetic per node as the flat kernel above, in the layout's element order.
 // Chunks of tsy * tsz elements are one tile's patch of one x-plane; a vector
 // of W elements never straddles a chunk (tsy * tsz * sizeof(T) is a multiple
-// of 16 bytes, checked by the host wrapper).
-template <typename T>
+// of 16 bytes, checked by the host wrapper).  ROW: tsz is a multiple of W as
+// well, so a vector lies in one z-row of its chunk and its position, owned
+// mask and y-interface term are resolved once per vector instead of once per
+// element.  Used for FP32 (4 elements per 16-byte vector): Q6 FP32 update
+// 1.58 -> 1.41 ms, +3 % GDoF/s; FP64 keeps the per-element form (ROW: Q3
+// update 1.555 -> 1.583 ms), same box (scripts/r3_updrow.sh).
+template <typename T, bool ROW>
 __global__ void __launch_bounds__(256)
     cg_update_tiled_kernel(int64_t L0, int64_t L1, int64_t Lz, int tsy, int tsz, int tntz,
                            int64_t o0, int64_t o1, int64_t o2, int64_t nvec, T* __restrict__ r,
@@ -144,35 +149,65 @@ __global__ void __launch_bounds__(256)
     if (x >= o0) continue;
     const int ein = static_cast<int>(e0 - c * ch);
     if (BDX_OOB(e0 + W - 1, nvec * W, "tiled update")) continue;
-    const V vy = *reinterpret_cast<const V*>(y + e0);
-    V vr = *reinterpret_cast<const V*>(r + e0);
-    bool any = false;
-    // (y, z) of the chunk's first element once; the others step along z
+    // (y, z) of the vector's first element
     int ly = static_cast<int>(static_cast<float>(ein) * inv_tsz);
     if (ly * tsz > ein) --ly;
     if ((ly + 1) * tsz <= ein) ++ly;
-    int lz = ein - ly * tsz - 1;
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      if (++lz == tsz) {
-        lz = 0;
-        ++ly;
-      }
-      const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz = static_cast<int64_t>(tZ) * tsz + lz;
-      if (gy >= o1 || gz >= o2) continue;
-      any = true;
+    if constexpr (ROW) {
+      const int lz0 = ein - ly * tsz;
+      const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz0 = static_cast<int64_t>(tZ) * tsz + lz0;
+      if (gy >= o1 || gz0 >= o2) continue;
+      V t = *reinterpret_cast<const V*>(y + e0);
+      V vr = *reinterpret_cast<const V*>(r + e0);
       const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
-      T t = vy[w];
-      if (yrow >= 0) t += yb[(x * (nty - 1) + yrow) * Lz + gz];
-      if (lz == 0 && tZ >= 1 && tZ < ntz) {
-        t += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
-        if (yrow >= 0) t += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
+      const int nw = o2 - gz0 < W ? static_cast<int>(o2 - gz0) : W;  // owned elements
+      if (yrow >= 0) {
+        const T* yr = yb + (x * (nty - 1) + yrow) * Lz + gz0;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (w < nw) t[w] += yr[w];
       }
-      const T rn = vr[w] - alpha * t;
-      vr[w] = rn;
-      acc += static_cast<double>(rn) * static_cast<double>(rn);
+      if (lz0 == 0 && tZ >= 1 && tZ < ntz) {
+        t[0] += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
+        if (yrow >= 0) t[0] += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const T rn = vr[w] - alpha * t[w];
+        if (w < nw) {
+          vr[w] = rn;
+          acc += static_cast<double>(rn) * static_cast<double>(rn);
+        }
+      }
+      *reinterpret_cast<V*>(r + e0) = vr;
+    } else {
+      const V vy = *reinterpret_cast<const V*>(y + e0);
+      V vr = *reinterpret_cast<const V*>(r + e0);
+      bool any = false;
+      // the other elements step along z
+      int lz = ein - ly * tsz - 1;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        if (++lz == tsz) {
+          lz = 0;
+          ++ly;
+        }
+        const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz = static_cast<int64_t>(tZ) * tsz + lz;
+        if (gy >= o1 || gz >= o2) continue;
+        any = true;
+        const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
+        T t = vy[w];
+        if (yrow >= 0) t += yb[(x * (nty - 1) + yrow) * Lz + gz];
+        if (lz == 0 && tZ >= 1 && tZ < ntz) {
+          t += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
+          if (yrow >= 0) t += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
+        }
+        const T rn = vr[w] - alpha * t;
+        vr[w] = rn;
+        acc += static_cast<double>(rn) * static_cast<double>(rn);
+      }
+      if (any) *reinterpret_cast<V*>(r + e0) = vr;
     }
-    if (any) *reinterpret_cast<V*>(r + e0) = vr;
   }
   const double t = block_sum(acc, lds);
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
@@ -274,10 +309,16 @@ BDX_CGI(float, f32)
     const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
     const int64_t want = (nvec + 255) / 256;                                                   \
     const int g = static_cast<int>(want < kUpdGrid ? (want > 0 ? want : 1) : kUpdGrid); \
-    cg_update_tiled_kernel<T><<<g, 256, 0, st>>>(                                              \
-        L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),              \
-        static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,    \
-        scal, rn_slot, pap_slot, partials);                                                    \
+    if (sizeof(T) == 4 && L.tsz % 4 == 0)                                                      \
+      cg_update_tiled_kernel<T, true><<<g, 256, 0, st>>>(                                      \
+          L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),            \
+          static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,  \
+          scal, rn_slot, pap_slot, partials);                                                  \
+    else                                                                                       \
+      cg_update_tiled_kernel<T, false><<<g, 256, 0, st>>>(                                     \
+          L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),            \
+          static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,  \
+          scal, rn_slot, pap_slot, partials);                                                  \
     if (g > 4 * kStage1) {                                                                     \
       double* stage = partials + kPartialsCap - kStage1;                                       \
       reduce_partials_slices<<<kStage1, 256, 0, st>>>(partials, g, stage);                     \
