@@ -118,7 +118,9 @@ __global__ void __launch_bounds__(256)
 // mask and y-interface term are resolved once per vector instead of once per
 // element.  Used for FP32 (4 elements per 16-byte vector): Q6 FP32 update
 // 1.58 -> 1.41 ms, +3 % GDoF/s; FP64 keeps the per-element form (ROW: Q3
-// update 1.555 -> 1.583 ms), same box (scripts/r3_updrow.sh).
+// update 1.555 -> 1.583 ms), same box (scripts/r3_updrow.sh).  Blocks stay in
+// launch order: an XCD-aware remap (contiguous slabs per XCD) made the pass
+// 8-40 % slower (Q6 FP64 update 2.54 -> 3.54 ms, scripts/r3_updxcd.sh).
 template <typename T, bool ROW>
 __global__ void __launch_bounds__(256)
     cg_update_tiled_kernel(int64_t L0, int64_t L1, int64_t Lz, int tsy, int tsz, int tntz,
