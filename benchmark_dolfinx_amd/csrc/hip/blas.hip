@@ -187,56 +187,59 @@ __global__ void __launch_bounds__(kBlock)
 // iterate and the result exported to the lattice layout in one pass
 // (t += a1 p1 [+ a2 p2]; lat = t) instead of a flush pass per term plus a
 // conversion pass.  a = scal[num] / scal[den], den < 0: scal[num] itself.
-// The pass walks the tiled side ([tile][x][ly][lz], three of its four
-// streams) in 16-byte vectors and scatters each vector's elements to their
-// lattice z-runs; chunk / tile / row positions come from reciprocal
-// multiplies with a correction step (as the tiled r update), not 64-bit
-// divisions per element (those made the lattice-order form ALU-bound at
-// ~2 TB/s).  Requires tsy * tsz * sizeof(T) % 16 == 0 (host check).
+// One block per (x-plane, tile row, group of kFeTiles tiles along z): it
+// reads the group's tiled chunks ([tile][x][ly][lz], contiguous) in 16-byte
+// vectors, stages the result in LDS in lattice order and writes the group's
+// z-rows contiguously, so both sides stream (the element-wise forms ran at
+// 2-3.7 TB/s: 64-bit divisions per element, then 96-byte lattice runs).
+constexpr int kFeTiles = 16;
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
     flush_export_kernel(int64_t L0, int64_t L1, int64_t L2, int64_t ld, int tsy, int tsz,
-                        int tntz, int64_t nvec, T* __restrict__ a, T* __restrict__ t,
+                        int tntz, int ngz, T* __restrict__ a, T* __restrict__ t,
                         const T* __restrict__ p1, const T* __restrict__ p2,
                         const double* __restrict__ scal, int num1, int den1, int num2, int den2) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fe_lds[];
+  T* const sv = reinterpret_cast<T*>(fe_lds);  // [tsy][kFeTiles * tsz]
   const T a1 = static_cast<T>(den1 < 0 ? scal[num1] : scal[num1] / scal[den1]);
   const T a2 = p2 ? static_cast<T>(den2 < 0 ? scal[num2] : scal[num2] / scal[den2]) : T(0);
   constexpr int W = 16 / sizeof(T);
   typedef T V __attribute__((ext_vector_type(W)));
-  const int64_t ch = static_cast<int64_t>(tsy) * tsz;  // one tile's patch of one x-plane
-  const double inv_ch = 1.0 / static_cast<double>(ch), inv_l0 = 1.0 / static_cast<double>(L0);
-  const float inv_tsz = 1.0f / static_cast<float>(tsz);
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * kBlock) {
-    const int64_t e0 = v * W;
-    int64_t c = static_cast<int64_t>(static_cast<double>(e0) * inv_ch);  // chunk = tile * L0 + x
-    if (c * ch > e0) --c;
-    if ((c + 1) * ch <= e0) ++c;
-    int64_t blk = static_cast<int64_t>(static_cast<double>(c) * inv_l0);  // tile
-    if (blk * L0 > c) --blk;
-    if ((blk + 1) * L0 <= c) ++blk;
-    const int64_t x = c - blk * L0;
-    const int tY = static_cast<int>(blk / tntz), tZ = static_cast<int>(blk - static_cast<int64_t>(tY) * tntz);
-    const int ein = static_cast<int>(e0 - c * ch);
-    int ly = static_cast<int>(static_cast<float>(ein) * inv_tsz);
-    if (ly * tsz > ein) --ly;
-    if ((ly + 1) * tsz <= ein) ++ly;
-    int lz = ein - ly * tsz - 1;
-    if (BDX_OOB(e0 + W - 1, nvec * W, "flush export")) continue;
-    V vt = *reinterpret_cast<const V*>(t + e0);
-    const V v1 = *reinterpret_cast<const V*>(p1 + e0);
-    vt += a1 * v1;
-    if (p2) vt += a2 * *reinterpret_cast<const V*>(p2 + e0);
-    *reinterpret_cast<V*>(t + e0) = vt;
+  // block -> (x, tile row ty, z group g); x fastest
+  const int64_t bidx = blockIdx.x;
+  const int64_t x = bidx % L0, rest = bidx / L0;
+  const int g = static_cast<int>(rest % ngz), ty = static_cast<int>(rest / ngz);
+  const int tz0 = g * kFeTiles;
+  const int nt = tntz - tz0 < kFeTiles ? tntz - tz0 : kFeTiles;  // tiles of this group
+  const int C = tsy * tsz, CV = C / W;                              // chunk, vectors per chunk
+  const int pitch = kFeTiles * tsz;                                 // LDS row pitch
+  const int64_t cbase = (static_cast<int64_t>(ty) * tntz + tz0) * L0 + x;  // chunk index of tile tz0
+  for (int q = threadIdx.x; q < nt * CV; q += kBlock) {
+    const int tl = q / CV, e = (q - tl * CV) * W;
+    const int64_t off = (cbase + static_cast<int64_t>(tl) * L0) * C + e;
+    V vt = *reinterpret_cast<const V*>(t + off);
+    vt += a1 * *reinterpret_cast<const V*>(p1 + off);
+    if (p2) vt += a2 * *reinterpret_cast<const V*>(p2 + off);
+    *reinterpret_cast<V*>(t + off) = vt;
+    int ly = e / tsz, lz = e - ly * tsz;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
+      sv[ly * pitch + tl * tsz + lz] = vt[w];
       if (++lz == tsz) {
         lz = 0;
         ++ly;
       }
-      const int64_t j = static_cast<int64_t>(tY) * tsy + ly, k = static_cast<int64_t>(tZ) * tsz + lz;
-      if (j < L1 && k < L2) a[(x * L1 + j) * ld + k] = vt[w];
     }
+  }
+  __syncthreads();
+  const int64_t k0 = static_cast<int64_t>(tz0) * tsz;
+  const int64_t kend = (k0 + nt * tsz < L2) ? k0 + nt * tsz : L2;
+  const int nk = static_cast<int>(kend - k0);
+  const int64_t j0 = static_cast<int64_t>(ty) * tsy;
+  const int nj = static_cast<int>((j0 + tsy <= L1) ? tsy : L1 - j0);
+  for (int r = threadIdx.x; r < nj * nk; r += kBlock) {
+    const int ly = r / nk, kk = r - ly * nk;
+    a[(x * L1 + j0 + ly) * ld + k0 + kk] = sv[ly * pitch + kk];
   }
 }
 
@@ -350,14 +353,16 @@ int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
     const BdxLattice L = BdxLattice::from(latd_tiled);                        \
     if (!L.tsy || (L.tsy * L.tsz * static_cast<int64_t>(sizeof(T))) % 16)    \
       return static_cast<int>(hipErrorInvalidValue);                          \
-    /* the tiled storage: ceil(L1 / tsy) * tntz tiles of tcol elements */     \
-    const int64_t nt = ((L.L[1] - 1) / L.tsy + 1) * L.tntz * L.tcol;          \
-    const int64_t nvec = nt / (16 / static_cast<int64_t>(sizeof(T)));         \
-    const int64_t g64 = (nvec + kBlock - 1) / kBlock;                         \
-    const int g = static_cast<int>(g64 < 65536 ? g64 : 65536);                \
-    flush_export_kernel<T><<<g, kBlock, 0, st>>>(                             \
+    const int64_t nty = (L.L[1] - 1) / L.tsy + 1;                             \
+    const int ngz = static_cast<int>((L.tntz + kFeTiles - 1) / kFeTiles);     \
+    const int64_t nblk = L.L[0] * nty * ngz;                                  \
+    const size_t lds = static_cast<size_t>(L.tsy) * kFeTiles * L.tsz * sizeof(T); \
+    if (nblk <= 0) return 0;                                                  \
+    if (nblk > 0x7fffffffLL || lds > 64 * 1024)                               \
+      return static_cast<int>(hipErrorInvalidValue);                          \
+    flush_export_kernel<T><<<static_cast<unsigned>(nblk), kBlock, lds, st>>>( \
         L.L[0], L.L[1], L.L[2], L.ld, static_cast<int>(L.tsy),                \
-        static_cast<int>(L.tsz), static_cast<int>(L.tntz), nvec, lat, tiled,  \
+        static_cast<int>(L.tsz), static_cast<int>(L.tntz), ngz, lat, tiled,   \
         p1, p2, scal, num1, den1, num2, den2);                                \
     return static_cast<int>(hipGetLastError());                               \
   }
