@@ -700,6 +700,7 @@ static __global__ void __launch_bounds__(256)
 
 // CG update of the dofmap path: alpha = s[rn] / s[pap]; r -= alpha y over
 // every local dof, r.r over the owned ones, y = 0 for the next operator.
+// 16-byte vectors (and W flag bytes) per thread; block 0 takes the tail.
 template <typename T>
 __global__ void __launch_bounds__(256)
     dofmap_cg_update_kernel(int64_t n, const unsigned char* __restrict__ flags, T* __restrict__ r,
@@ -707,13 +708,28 @@ __global__ void __launch_bounds__(256)
                             int pap_slot, double* __restrict__ partials) {
   __shared__ double lds[16];
   const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
+  constexpr int W = 16 / sizeof(T);
+  typedef T V __attribute__((ext_vector_type(W)));
+  typedef unsigned char F __attribute__((ext_vector_type(W)));
   double acc = 0.0;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const T rn = r[i] - alpha * y[i];
-    r[i] = rn;
-    y[i] = T(0);
-    if (flags[i] & 2u) acc += static_cast<double>(rn) * static_cast<double>(rn);
+  const int64_t nv = n / W;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv;
+       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const V rn = *reinterpret_cast<const V*>(r + v * W) - alpha * *reinterpret_cast<const V*>(y + v * W);
+    const F fl = *reinterpret_cast<const F*>(flags + v * W);
+    *reinterpret_cast<V*>(r + v * W) = rn;
+    *reinterpret_cast<V*>(y + v * W) = V(0);
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (fl[w] & 2u) acc += static_cast<double>(rn[w]) * static_cast<double>(rn[w]);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = nv * W + threadIdx.x; i < n; i += blockDim.x) {
+      const T rn = r[i] - alpha * y[i];
+      r[i] = rn;
+      y[i] = T(0);
+      if (flags[i] & 2u) acc += static_cast<double>(rn) * static_cast<double>(rn);
+    }
   }
   const double t = block_sum(acc, lds);
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
@@ -821,7 +837,7 @@ int launch_dofmap_geometry(int ncells, const int* cverts, const T* coords, const
   extern "C" int bdx_dofmap_cg_update_##SUF(int64_t n, const unsigned char* flags, T* r, T* y,    \
                                             const double* scal, int rn_slot, int pap_slot,        \
                                             double* partials, int* nblocks, hipStream_t st) {     \
-    const int64_t want = (n + 1023) / 1024;                                                       \
+    const int64_t want = (n / (16 / static_cast<int64_t>(sizeof(T))) + 1023) / 1024;              \
     const int g = static_cast<int>(want < kDofMaxBlocks ? (want > 0 ? want : 1) : kDofMaxBlocks); \
     dofmap_cg_update_kernel<T><<<g, 256, 0, st>>>(n, flags, r, y, scal, rn_slot, pap_slot,        \
                                                   partials);                                      \
