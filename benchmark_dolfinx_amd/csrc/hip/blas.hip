@@ -183,6 +183,8 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+constexpr int kFeTiles = 16;  // tiles per flush_export block along z
+
 // End of a CG call on tiled storage: the lagged x terms folded into the tiled
 // iterate and the result exported to the lattice layout in one pass
 // (t += a1 p1 [+ a2 p2]; lat = t) instead of a flush pass per term plus a
@@ -192,7 +194,6 @@ __global__ void __launch_bounds__(kBlock)
 // vectors, stages the result in LDS in lattice order and writes the group's
 // z-rows contiguously, so both sides stream (the element-wise forms ran at
 // 2-3.7 TB/s: 64-bit divisions per element, then 96-byte lattice runs).
-constexpr int kFeTiles = 16;
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
     flush_export_kernel(int64_t L0, int64_t L1, int64_t L2, int64_t ld, int tsy, int tsz,
