@@ -32,7 +32,9 @@
 //                             contiguous across these lanes), with the y- and
 //                             z-derivatives formed by lanes (qx, qz) / (qx, qy)
 // The stored-G loads of a cell are issued before its first contraction, so
-// they are in flight under the interpolation and gradient stages.
+// they are in flight under the interpolation and gradient stages (at Q3 as
+// 16-byte chunks of the cells' contiguous G blocks, redistributed to the
+// quadrature lanes through LDS).
 //
 // CG mode fuses the reference's BLAS-1 calls (src/cg.hpp:121-167) into the
 // gather: p = r + beta p_old is formed per gathered dof, the designated
@@ -101,11 +103,22 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   constexpr int ND3 = ND * ND * ND, NQ3 = NQ * NQ * NQ;
   constexpr bool IDENT = ND == NQ;  // qmode 0, GLL: phi0 = I (quirk Q5 guarantees it)
   constexpr bool GPREF = GEOM == kGeomStored && S::GPREF;
+  // GLDS: the prefetched stored G of the wave's cells moves as 16-byte
+  // chunks (each cell's G block is contiguous) and is redistributed to the
+  // quadrature lanes through LDS at the F stage: 12 instead of 30 load
+  // instructions per cell pair at Q3, 194 -> 140 VGPRs, +2.9 % same box
+  // (scripts/r3_dofglds.sh).  Two cells per wave (NQ = 5) only: with more
+  // cells per wave the 12-24 KB of staging per wave would cut the workgroups
+  // per CU below what the register version reaches.
+  constexpr int GE = CPW * 6 * NQ3;  // stored-G values of the wave's cells
+  constexpr bool GLDS = GPREF && CPW <= 2 && (6 * NQ3 * sizeof(T)) % 16 == 0;
+  constexpr int GW = 16 / sizeof(T), GCH = GLDS ? (GE / GW + 63) / 64 : 1;
   static_assert(ND * ND <= 64, "nodal z-lines: one per lane");
   __shared__ __attribute__((aligned(16))) T s_buf[S::WAVES][CPW][3][BUF];
   __shared__ T s_X[S::WAVES][CPW][24];
   __shared__ int s_ids[S::WAVES][2][64];  // per-wave ring of cell ids (two blocks)
   __shared__ double s_red[16];
+  __shared__ __attribute__((aligned(16))) T s_G[GLDS ? S::WAVES : 1][GLDS ? GE : GW];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int slot = CPW > 1 ? lane / NQ2 : 0;
@@ -256,9 +269,21 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     }
     g.kc = ldv(rs_kc, static_cast<unsigned>(c32) * sizeof(T));
   };
-  T Gr[LPL][GPREF ? 6 * NQ : 1];
-  auto load_G = [&](int c32) {
-    if constexpr (GPREF) {
+  T Gr[LPL][GPREF && !GLDS ? 6 * NQ : 1];
+  typedef T GV __attribute__((ext_vector_type(16 / sizeof(T))));
+  GV Gv[GCH];
+  auto load_G = [&](int j, int c32) {
+    if constexpr (GLDS) {
+#pragma unroll
+      for (int m = 0; m < GCH; ++m) {
+        const int e = (lane + 64 * m) * GW;  // first value of this lane's chunk
+        if (e < GE) {
+          const int s = e / (6 * NQ3);
+          Gv[m] = *reinterpret_cast<const GV*>(A.G + static_cast<int64_t>(cell_at(j, s)) * 6 * NQ3 +
+                                               (e - s * 6 * NQ3));
+        }
+      }
+    } else if constexpr (GPREF) {
       const T* Gc = A.G + static_cast<int64_t>(c32) * 6 * NQ3;
 #pragma unroll
       for (int rp = 0; rp < LPL; ++rp)
@@ -282,7 +307,7 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     load_dofs(0, dA);
     load_verts(cell_cur, vA);
     gather(dA, vA, 0, cell_cur, gc);
-    load_G(cell_cur);
+    load_G(0, cell_cur);
     load_dofs(1, dB);
     load_verts(cell_of(1), vB);
   }
@@ -469,6 +494,14 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
         }
       }
     } else {
+      if constexpr (GLDS) {
+#pragma unroll
+        for (int m = 0; m < GCH; ++m) {
+          const int e = (lane + 64 * m) * GW;
+          if (e < GE) *reinterpret_cast<GV*>(&s_G[wv][e]) = Gv[m];
+        }
+        dof_wave_sync();
+      }
 #pragma unroll
       for (int rp = 0; rp < LPL; ++rp) {
         const int a = qa_of(rp), b = qb_of(rp);
@@ -484,7 +517,9 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
           T Gd[6];
 #pragma unroll
           for (int k = 0; k < 6; ++k) {
-            if constexpr (GPREF)
+            if constexpr (GLDS)
+              Gd[k] = s_G[wv][(slot_on ? slot : 0) * 6 * NQ3 + k * NQ3 + qx * NQ2 + sl + 64 * rp];
+            else if constexpr (GPREF)
               Gd[k] = Gr[rp][k * NQ + qx];
             else
               Gd[k] = A.G[cell * 6 * NQ3 + k * NQ3 + qx * NQ2 + sl + 64 * rp];
@@ -619,7 +654,7 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       dof_wave_sync();  // the id ring entry of j + 1 / j + 2 is visible
       const int cn = cell_of(j + 1), cnn = cell_of(j + 2);
       gather(dn, vn, j + 1, cn, gc);
-      load_G(cn);
+      load_G(j + 1, cn);
       load_dofs(j + 2, dc);
       load_verts(cnn, vc);
       cell_cur = cn;
