@@ -35,6 +35,8 @@ import os
 import sys
 import time
 
+METRIC = "GDOF/s matrix-free Laplacian apply, Q3@300M & Q6@500M dofs/GPU, 1/2/4/8 MI355X"
+
 CONFIGS = {
     # name: (degree, dofs_per_gpu, float bits, baseline GDoF/s per GPU or None)
     "q3": (3, 300_000_000, 64, 4.024),
@@ -65,11 +67,12 @@ def parse_args(argv=None):
                     help="extra eager iterations with hipEvent phase timers (0: none)")
     ap.add_argument("--companions", default="auto", choices=["auto", "on", "off"],
                     help="after the Q3 headline, time the metric's second half (Q6 at 500 M "
-                         "DoFs/GPU, FP64 and FP32) with the same steps/warmup and report "
-                         "q6_gdofs / q6f32_gdofs (auto: on for the q3 config)")
+                         "DoFs/GPU, FP64 and FP32) and the headline with per-cell random "
+                         "coefficients, each with the same steps/warmup, and report q6_gdofs / "
+                         "q6f32_gdofs / random_kappa_gdofs (auto: on for the q3 config)")
     ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
-                    help="after the headline, time variants of it: per-cell random "
-                         "coefficients, the perturbed (general trilinear) mesh, the "
+                    help="after the headline, time variants of it: the perturbed "
+                         "(general trilinear) mesh, the "
                          "reference's data model (dofmap + stored G) and Q6 perturbed "
                          "(GPU only; auto: on for one rank)")
     return ap.parse_args(argv)
@@ -100,6 +103,9 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
     from benchmark_dolfinx_amd.models.poisson import PoissonProblem
     from benchmark_dolfinx_amd.solvers.cg import DeviceCG, cg_solve
 
+    fail = os.environ.get("BDX_BENCH_FAIL_MEASURE", "")  # test hook: "<config>[:<kappa>]"
+    if fail and fail in (config, f"{config}:{kappa}"):
+        raise RuntimeError(f"injected failure in the {config} measurement")
     degree, dpg, bits, base = CONFIGS[config]
     if a.dofs_per_gpu:
         dpg = a.dofs_per_gpu
@@ -134,9 +140,17 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
             torch.cuda.synchronize()
 
     cg = None
+    preflight = None
     if gpu:
         cg = DeviceCG(pb)
         cg.start(op, x, u)
+        rt0 = getattr(op, "_rt", None)
+        if rt0 is not None and n > 1:
+            # the first exchange and all-reduce of the runtime's own RCCL
+            # communicator, bounded well below the run deadline: a peer that
+            # never joins surfaces here as an error, not as a hung warmup
+            preflight = rt0.preflight(float(os.environ.get("BDX_PREFLIGHT_TIMEOUT_S", "120")))
+            log(f"{config}: pre-flight exchange + all-reduce {preflight['ms']:.1f} ms")
         cg.iterate(warmup)
         cg.wait()
     else:
@@ -199,6 +213,8 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
                  "graphs": rt.graphs if rt is not None else False,
                  "halo_overlap": rt.overlap if rt is not None else False,
                  "halo_bytes_per_exchange": pb.halo.bytes_per_exchange,
+                 "comm_stream_priority": rt.comm_priority() if rt is not None else None,
+                 "preflight_ms": preflight["ms"] if preflight else None,
                  "rank_ms_per_step_max": 1e3 * max(rank_dt) / steps,
                  "rank_ms_per_step_min": 1e3 * min(rank_dt) / steps},
     }
@@ -231,12 +247,28 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
     return rec
 
 
+class MeasurementFailed(RuntimeError):
+    """A measurement failed on a multi-rank run: fatal (the other ranks may
+    be inside a collective the failed rank will never join), but it carries
+    the records measured so far so rank 0 can still report them."""
+
+    def __init__(self, msg, partial):
+        super().__init__(msg)
+        self.partial = partial
+
+
 def _guarded(comm, fn, log) -> dict:
-    """Run one secondary measurement; an error is recorded, not raised, so
-    the already measured headline is always reported."""
+    """Run one secondary measurement.  On one rank an error is recorded, not
+    raised, so the already measured headline is always reported.  With
+    several ranks it is re-raised: a rank that skipped ahead would start the
+    next measurement while its peers are still inside the failed one's
+    collectives (they would block until the deadline or pair up the wrong
+    collectives)."""
     try:
         return fn()
     except Exception as e:  # noqa: BLE001 - reported in the JSON
+        if comm.size > 1:
+            raise
         log(f"secondary measurement failed: {e!r}")
         try:
             import torch
@@ -271,14 +303,22 @@ def run(comm, a) -> dict | None:
     head = _measure(comm, a, a.config, a.steps, a.warmup, kappa=a.kappa, perturb=a.perturb,
                     kernel=a.kernel, geometry=a.geometry, profile_steps=a.profile_steps,
                     log=log)
-    # the metric's second half: Q6 at 500 M DoFs/GPU, FP64 and FP32, on the
-    # same clock discipline as the headline (own steps / warmup / ms_per_step)
+    # the metric's second half (Q6 at 500 M DoFs/GPU, FP64 and FP32) and the
+    # north star's random coefficients on the headline config, each on the
+    # headline's clock discipline (own steps / warmup / ms_per_step), at
+    # every rank count
     companions = {}
     if a.companions == "on" or (a.companions == "auto" and a.config == "q3" and not a.mesh):
-        for c in ("q6", "q6f32"):
-            companions[c] = _guarded(comm, lambda c=c: _measure(
-                comm, a, c, a.steps, a.warmup, kappa=a.kappa, perturb=a.perturb,
-                kernel=a.kernel, geometry=a.geometry, log=log), log)
+        specs = [(c, c, a.kappa) for c in ("q6", "q6f32")]
+        if a.kappa == "constant":
+            specs.append(("random_kappa", a.config, "random"))
+        for key, c, kap in specs:
+            try:
+                companions[key] = _guarded(comm, lambda c=c, kap=kap: _measure(
+                    comm, a, c, a.steps, a.warmup, kappa=kap, perturb=a.perturb,
+                    kernel=a.kernel, geometry=a.geometry, log=log), log)
+            except Exception as e:
+                raise MeasurementFailed(f"{key}: {e!r}", (head, companions)) from e
     extras = {}
     if gpu and (a.extras == "on" or (a.extras == "auto" and n == 1)):
         # north-star variants of the headline config (BASELINE.json: random
@@ -290,8 +330,7 @@ def run(comm, a) -> dict | None:
         # stored per quadrature point, as the reference does.
         vsteps = min(a.steps, 50)
         pert = a.perturb or 0.1
-        specs = (("random_kappa", a.config, dict(kappa="random", perturb=a.perturb)),
-                 ("general", a.config, dict(kappa=a.kappa, perturb=pert)),
+        specs = (("general", a.config, dict(kappa=a.kappa, perturb=pert)),
                  ("general_trilinear", a.config, dict(kappa=a.kappa, perturb=pert,
                                                       geometry="otf-general")),
                  ("dofmap", a.config, dict(kappa=a.kappa, perturb=a.perturb, kernel="dofmap",
@@ -306,11 +345,15 @@ def run(comm, a) -> dict | None:
                 comm, a, cfg, vsteps, 3, log=log, **kw), log)
     if comm.rank != 0:
         return None
+    return _record(a, n, head, companions, extras, flags, gpu)
+
+
+def _record(a, n, head, companions, extras, flags, gpu) -> dict:
+    """Rank 0's JSON line."""
     degree = head["degree"]
     px, py, pz = head["partition"]
     return {
-        "metric": "GDOF/s matrix-free Laplacian apply, Q3@300M & Q6@500M dofs/GPU, "
-                  "1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": head["value"],
         "unit": "GDoF/s",
         "n_gpus": n,
@@ -352,7 +395,7 @@ def run(comm, a) -> dict | None:
         "q6_gdofs": companions.get("q6", {}).get("value"),
         "q6f32_gdofs": companions.get("q6f32", {}).get("value"),
         "companions": companions,
-        "random_kappa_gdofs": extras.get("random_kappa", {}).get("value"),
+        "random_kappa_gdofs": companions.get("random_kappa", {}).get("value"),
         "general_gdofs": extras.get("general", {}).get("value"),
         "general_trilinear_gdofs": extras.get("general_trilinear", {}).get("value"),
         "dofmap_gdofs": extras.get("dofmap", {}).get("value"),
@@ -431,8 +474,12 @@ def launch_ranks(n: int, argv: list[str], port: int | None = None,
             procs.append(subprocess.Popen([sys.executable, script, *argv], env=env, stdout=out,
                                           text=True, preexec_fn=_deathsig))
 
+        relayed = []
+
         def _relay(stream):
             for line in stream:
+                if line.startswith("{"):
+                    relayed.append(line)
                 sys.stdout.write(line)
                 sys.stdout.flush()
 
@@ -452,7 +499,15 @@ def launch_ranks(n: int, argv: list[str], port: int | None = None,
                 break
             time.sleep(poll_s)
         relay.join(timeout=10)
-        return rc if rc >= 0 else 128 - rc
+        rc = rc if rc >= 0 else 128 - rc
+        if rc and not relayed:
+            # rank 0 never got to report (it was taken down with a failed
+            # peer): the one JSON line says so instead of leaving stdout empty
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GDoF/s", "n_gpus": n,
+                              "higher_is_better": True, "scaling": "weak",
+                              "error": f"a rank exited with {rc} before rank 0 reported"}),
+                  flush=True)
+        return rc
     finally:
         for s_, h in old.items():
             signal.signal(s_, h)
@@ -475,7 +530,26 @@ def main(argv=None) -> int:
     from benchmark_dolfinx_amd.parallel.comm import finalize, init_distributed
 
     comm = init_distributed(a.platform)
-    line = run(comm, a)
+    try:
+        line = run(comm, a)
+    except Exception as e:
+        # one JSON line with the error (and whatever was measured before it)
+        # instead of a silent non-zero exit; the process still fails
+        if comm.rank == 0:
+            rec = {"metric": METRIC, "value": None, "unit": "GDoF/s", "n_gpus": a.gpus,
+                   "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+                   "scaling": "weak", "error": repr(e)}
+            part = getattr(e, "partial", None)
+            if part is not None:
+                try:
+                    rec.update(_record(a, comm.size, part[0], part[1], {}, None,
+                                       a.platform == "gpu"))
+                    rec["error"] = repr(e)
+                except Exception:  # noqa: BLE001 - the error line must go out
+                    pass
+            print(json.dumps(rec), flush=True)
+        print(f"bench.py: rank {comm.rank}: {e!r}", file=sys.stderr, flush=True)
+        return 1
     if line is not None:
         print(json.dumps(line), flush=True)
     finalize()

@@ -713,24 +713,24 @@ __global__ void __launch_bounds__(256)
 // `cells`, position p = list index * ND^3 + local dof) of every dof.
 static __global__ void __launch_bounds__(256)
     dofmap_first_kernel(const int* __restrict__ cells, int ncl, const int* __restrict__ cdofs,
-                        int nd3, int pos0, unsigned* __restrict__ first) {
+                        int nd3, unsigned pos0, unsigned* __restrict__ first) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= static_cast<int64_t>(ncl) * nd3) return;
   const int64_t li = t / nd3;
   const int loc = static_cast<int>(t - li * nd3);
   const int d = cdofs[static_cast<int64_t>(cells[li]) * nd3 + loc] & 0x7fffffff;
-  atomicMin(first + d, static_cast<unsigned>(pos0 + t));
+  atomicMin(first + d, pos0 + static_cast<unsigned>(t));
 }
 static __global__ void __launch_bounds__(256)
     dofmap_mark_kernel(const int* __restrict__ cells, int ncl, int* __restrict__ cdofs, int nd3,
-                       int pos0, const unsigned* __restrict__ first) {
+                       unsigned pos0, const unsigned* __restrict__ first) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= static_cast<int64_t>(ncl) * nd3) return;
   const int64_t li = t / nd3;
   const int loc = static_cast<int>(t - li * nd3);
   int* e = cdofs + static_cast<int64_t>(cells[li]) * nd3 + loc;
   const int d = *e & 0x7fffffff;
-  *e = (first[d] == static_cast<unsigned>(pos0 + t)) ? (d | static_cast<int>(0x80000000u)) : d;
+  *e = (first[d] == pos0 + static_cast<unsigned>(t)) ? (d | static_cast<int>(0x80000000u)) : d;
 }
 
 // CG update of the dofmap path: alpha = s[rn] / s[pap]; r -= alpha y over

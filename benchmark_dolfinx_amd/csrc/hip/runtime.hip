@@ -38,6 +38,7 @@
 // (r0 = b - A x0, rho0) and hands the device buffers to this runtime.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -417,7 +418,11 @@ template <typename T>
 struct CGRuntime {
   RtConfig cfg;
   std::unique_ptr<Transport> tr;
-  int nranks = 1;
+  int nranks = 1, rank = 0;
+  // comm stream priority (hipDeviceGetStreamPriorityRange: least, greatest;
+  // the priority cs was created with)
+  int prio_least = 0, prio_greatest = 0, prio_cs = 0;
+  double* pf_scal = nullptr;  // pre-flight all-reduce slot
   // own non-blocking streams (graph capture is not allowed on the legacy
   // default stream torch may be using); ordered against the caller's stream
   // `ext` with events at the start and end of every iterate()
@@ -526,20 +531,26 @@ struct CGRuntime {
   }
   void advance_pend(int xm) { pend = (pend == 0 || xm == kXPair) ? 1 : (xm == kXSave ? 2 : 1); }
 
+  // The fused operator of iteration k on the tile rectangle `rect` (null:
+  // every tile) on stream s.
+  int launch_op(long k, bool first, bool xlag, int xm, const int* rect, hipStream_t s) {
+    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
+    T* pold = (k % 2 == 0) ? wpa : wpb;
+    T* pnew = (k % 2 == 0) ? wpb : wpa;
+    return apply(1 | (xm << 4) | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(),
+                 cfg.qpts.data(), wr, pold, pnew, wx, wy, yb, zb, cb, xv, kc, tabs, cfg.kappa,
+                 scal, partials, first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
+                 xlag ? kPAP : -1, cfg.nty, cfg.ntz, rect, s);
+  }
+
   // One CG iteration with explicit parity / flags (stream-ordered, no sync).
   // xm: kXSingle (pend 0: no x term; else alpha_prev p_old), kXSave, kXPair.
   int step(long k, bool first, bool xlag, int xm) {
     const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
-    T* pold = (k % 2 == 0) ? wpa : wpb;
-    T* pnew = (k % 2 == 0) ? wpb : wpa;
     T* const r = wr;
-    T* const x = wx;
     T* const y = wy;
     auto op = [&](const int* rect, hipStream_t s) {
-      return apply(1 | (xm << 4) | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(), cfg.qpts.data(), r, pold,
-                   pnew, x, y, yb, zb, cb, xv, kc, tabs, cfg.kappa, scal, partials,
-                   first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1, xlag ? kPAP : -1,
-                   cfg.nty, cfg.ntz, rect, s);
+      return launch_op(k, first, xlag, xm, rect, s);
     };
     int rc;
     mark(kMStart, st);
@@ -768,7 +779,9 @@ struct CGRuntime {
       };
       out[0] += dt(kMFwdBeg, kMFwdEnd);
       out[1] += dt(kMStart, kMOpA);
-      out[2] += dt(kMFwdEnd, kMBnd);
+      // split: forward-halo end -> boundary tiles + ghost fold; serial: the
+      // ghost fold only (kMFwdEnd precedes the whole operator there)
+      out[2] += split ? dt(kMFwdEnd, kMBnd) : dt(kMOpA, kMBnd);
       out[3] += dt(kMRevBeg, kMRevEnd);
       out[4] += dt(kMOpA, kMJoin);
       out[5] += dt(kMJoin, kMPap);
@@ -791,6 +804,128 @@ struct CGRuntime {
   }
   static constexpr int kNPhases = 13;
 
+  // Pre-flight of the transport before any timed work (bench.py at N > 1):
+  // one forward halo exchange of r and a device all-reduce of (rank + 1),
+  // under a deadline of timeout_s instead of the run's.  out[0] = host ms
+  // of both, out[1] = the all-reduce result (n (n + 1) / 2 when every rank
+  // took part).  A peer that never joins aborts the communicator: the error
+  // comes back here instead of a hang inside the warmup.
+  int preflight(double timeout_s, double* out) {
+    if (!pf_scal) BDX_CHECK(hipMalloc(&pf_scal, sizeof(double)));
+    const double v = rank + 1.0;
+    bdx::Watchdog* wd = tr->watchdog();
+    const double old = wd ? wd->timeout_s() : 0.0;
+    if (wd && timeout_s > 0) wd->set_timeout(timeout_s);
+    struct Restore {
+      bdx::Watchdog* w;
+      double t;
+      ~Restore() {
+        if (w) w->set_timeout(t);
+      }
+    } restore{wd, old};
+    BDX_CHECK(hipEventRecord(ev_in, ext));
+    BDX_CHECK(hipStreamWaitEvent(st, ev_in, 0));
+    const int64_t t0 = bdx::Watchdog::now_ns();
+    int rc = 0;
+    {
+      bdx::Watchdog::Busy busy(wd);
+      BDX_CHECK(hipMemcpyAsync(pf_scal, &v, sizeof(double), hipMemcpyHostToDevice, st));
+      if (halo) rc = halo_forward(wr, st);
+      if (!rc && nranks > 1) rc = tr->allreduce_sum(pf_scal, 1, st);
+      if (!rc) rc = static_cast<int>(hipEventRecord(ev_out, st));
+    }
+    if (!rc) rc = tr->wait(ev_out);
+    if (rc) return rc;
+    out[0] = (bdx::Watchdog::now_ns() - t0) * 1e-6;
+    BDX_CHECK(hipMemcpy(&out[1], pf_scal, sizeof(double), hipMemcpyDeviceToHost));
+    BDX_CHECK(hipStreamWaitEvent(ext, ev_out, 0));
+    return 0;
+  }
+
+  // Overlap probe (one rank only): does a comm-stream chain get CUs while the
+  // interior launch fills the chip?  The chain of the split schedule of a
+  // rank with y and z ghost planes (the N = 8 1 x 2 x 4 split) is replayed
+  // on cs with a 1-rank RCCL communicator: grouped self send/recv of n
+  // doubles (buf[0, n) -> buf[n, 2n)), the last tile row and column, the
+  // reverse send/recv; concurrently st runs the interior tile rectangle.
+  // out (ms, medians over reps): 0 chain alone, 1 interior alone, 2 chain
+  // done and 3 interior done measured from the common fork, 4 one exchange
+  // alone.  The CG state is clobbered: the caller restarts CG afterwards.
+  int overlap_probe(int64_t n, double* buf, int reps, double* out) {
+    if (nranks != 1 || cfg.nty < 2 || cfg.ntz < 2 || n <= 0 || reps <= 0)
+      return static_cast<int>(hipErrorInvalidValue);
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -10;
+    RcclTransport t;
+    if (t.connect(id, 1, 0)) return -11;
+    const std::vector<int64_t> cnt{n}, off0{0}, offn{n};
+    auto xchg = [&](hipStream_t s) {
+      return t.exchange(buf, cnt, off0, buf, cnt, offn, sizeof(double), s);
+    };
+    const int iy = cfg.nty - 1, iz = cfg.ntz - 1;
+    const int ra[4] = {0, iy, 0, iz}, r1[4] = {iy, cfg.nty, 0, cfg.ntz}, r2[4] = {0, iy, iz, cfg.ntz};
+    auto chain = [&](hipStream_t s) {
+      int rc = xchg(s);
+      if (!rc) rc = launch_op(0, true, false, kXSingle, r1, s);
+      if (!rc) rc = launch_op(0, true, false, kXSingle, r2, s);
+      if (!rc) rc = xchg(s);
+      return rc;
+    };
+    hipEvent_t e[4] = {};
+    for (auto& x : e) BDX_CHECK(hipEventCreate(&x));
+    struct Free {
+      hipEvent_t* e;
+      ~Free() {
+        for (int i = 0; i < 4; ++i)
+          if (e[i]) hipEventDestroy(e[i]);
+      }
+    } fr{e};
+    auto ms = [&](int a, int b) {
+      float v = 0.f;
+      (void)hipEventElapsedTime(&v, e[a], e[b]);
+      return static_cast<double>(v);
+    };
+    BDX_CHECK(hipDeviceSynchronize());
+    int rc = chain(cs);  // warm-up: RCCL connection setup, first launches
+    if (!rc) rc = launch_op(0, true, false, kXSingle, ra, st);
+    if (rc) return rc;
+    BDX_CHECK(hipDeviceSynchronize());
+    std::vector<double> v[5];
+    bdx::Watchdog::Busy busy(t.watchdog());
+    for (int it = 0; it < reps; ++it) {
+      // alone: the chain, the interior, one exchange
+      BDX_CHECK(hipEventRecord(e[0], cs));
+      if ((rc = chain(cs))) return rc;
+      BDX_CHECK(hipEventRecord(e[1], cs));
+      BDX_CHECK(hipEventRecord(e[2], st));
+      if ((rc = launch_op(0, true, false, kXSingle, ra, st))) return rc;
+      BDX_CHECK(hipEventRecord(e[3], st));
+      BDX_CHECK(hipDeviceSynchronize());
+      v[0].push_back(ms(0, 1));
+      v[1].push_back(ms(2, 3));
+      BDX_CHECK(hipEventRecord(e[0], cs));
+      if ((rc = xchg(cs))) return rc;
+      BDX_CHECK(hipEventRecord(e[1], cs));
+      BDX_CHECK(hipDeviceSynchronize());
+      v[4].push_back(ms(0, 1));
+      // together, enqueued in the runtime's order: fork, cs chain, st interior
+      BDX_CHECK(hipEventRecord(e[0], st));
+      BDX_CHECK(hipStreamWaitEvent(cs, e[0], 0));
+      if ((rc = chain(cs))) return rc;
+      BDX_CHECK(hipEventRecord(e[1], cs));
+      if ((rc = launch_op(0, true, false, kXSingle, ra, st))) return rc;
+      BDX_CHECK(hipEventRecord(e[2], st));
+      BDX_CHECK(hipDeviceSynchronize());
+      v[2].push_back(ms(0, 1));
+      v[3].push_back(ms(0, 2));
+    }
+    for (int i = 0; i < 5; ++i) {
+      std::sort(v[i].begin(), v[i].end());
+      out[i] = v[i][v[i].size() / 2];
+    }
+    return 0;
+  }
+
   ~CGRuntime() {
     drop_graphs();
     for (auto& e : pev)
@@ -800,6 +935,7 @@ struct CGRuntime {
       if (e) hipEventDestroy(e);
     if (st) hipStreamDestroy(st);
     if (cs) hipStreamDestroy(cs);
+    if (pf_scal) hipFree(pf_scal);
   }
 };
 
@@ -894,9 +1030,20 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   rt->ghost_total = halo_sizes[3];
   rt->nranks = nranks;
   rt->ext = st;
+  // The comm stream runs at the greatest priority the device offers: its
+  // chain (RCCL send/recv kernels, the boundary tiles, the ghost fold) is
+  // dispatched ahead of the interior launch's queued workgroups as soon as
+  // resident ones retire, instead of after the whole interior grid.
+  if (hipDeviceGetStreamPriorityRange(&rt->prio_least, &rt->prio_greatest) != hipSuccess) {
+    (void)hipGetLastError();
+    rt->prio_least = rt->prio_greatest = 0;
+  }
   if (hipStreamCreateWithFlags(&rt->st, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&rt->cs, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithPriority(&rt->cs, hipStreamNonBlocking, rt->prio_greatest) !=
+          hipSuccess ||
+      hipStreamGetPriority(rt->cs, &rt->prio_cs) != hipSuccess)
     return nullptr;
+  rt->rank = rank;
   for (hipEvent_t* e : {&rt->ev_in, &rt->ev_out, &rt->ev_fork,
                         &rt->ev_rev, &rt->ev_batch[0], &rt->ev_batch[1]})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
@@ -1026,6 +1173,28 @@ void* bdx_rt_create(int is_f64, const int64_t* latd, const int64_t* own, const i
                           tptrs);
   return create<float>(latd, own, iparams, kappa, wts, qpts, tabs, ptrs, halo_sizes, face_cnt,
                        ghost_cnt, transport, nranks, rank, group_id, st, latd_tiled, tptrs);
+}
+
+// Comm stream priority: out[0] least, out[1] greatest (device range),
+// out[2] the priority the comm stream runs at.
+int bdx_rt_comm_priority(void* h, int* out) {
+  return with_rt(h, [&](auto* rt) {
+    out[0] = rt->prio_least;
+    out[1] = rt->prio_greatest;
+    out[2] = rt->prio_cs;
+    return 0;
+  });
+}
+
+// Transport pre-flight (see CGRuntime::preflight); out[2].
+int bdx_rt_preflight(void* h, double timeout_s, double* out) {
+  return with_rt(h, [&](auto* rt) { return rt->preflight(timeout_s, out); });
+}
+
+// Comm/compute overlap probe on one GPU (see CGRuntime::overlap_probe);
+// buf: 2 n doubles; out[5].
+int bdx_rt_overlap_probe(void* h, int64_t n, double* buf, int reps, double* out) {
+  return with_rt(h, [&](auto* rt) { return rt->overlap_probe(n, buf, reps, out); });
 }
 
 // 1 if the loop runs on the tiled storage layout.

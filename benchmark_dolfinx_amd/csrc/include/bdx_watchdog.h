@@ -67,8 +67,8 @@ class Watchdog {
   // has exceeded the deadline or the communicator reports an error.
   bool check(int64_t t) {
     if (fired_.load()) return true;
-    const int64_t b = busy_since_.load();
-    const bool late = b != 0 && timeout_ns_ > 0 && t - b > timeout_ns_;
+    const int64_t b = busy_since_.load(), lim = timeout_ns_.load();
+    const bool late = b != 0 && lim > 0 && t - b > lim;
     const bool err = poll_error_ && poll_error_();
     if (!(late || err)) return false;
     bool expected = false;
@@ -97,10 +97,13 @@ class Watchdog {
 
   bool fired() const { return fired_.load(); }
   int reason() const { return reason_.load(); }  // 0 none, 1 deadline, 2 async error
-  double timeout_s() const { return timeout_ns_ * 1e-9; }
+  double timeout_s() const { return timeout_ns_.load() * 1e-9; }
+  // A shorter (or longer) deadline for the scopes opened from now on (the
+  // bench pre-flight bounds its first exchange far below the run deadline).
+  void set_timeout(double timeout_s) { timeout_ns_.store(static_cast<int64_t>(timeout_s * 1e9)); }
 
  private:
-  int64_t timeout_ns_;
+  std::atomic<int64_t> timeout_ns_;
   std::function<bool()> poll_error_;
   std::function<void()> on_fire_;
   std::atomic<int64_t> busy_since_{0};

@@ -81,6 +81,9 @@ def declare(lib) -> None:
     _d(lib, "bdx_rt_connect", [vp, vp, i32])
     _d(lib, "bdx_rt_comm_count", [vp])
     _d(lib, "bdx_rt_overlap", [vp])
+    _d(lib, "bdx_rt_comm_priority", [vp, vp])
+    _d(lib, "bdx_rt_preflight", [vp, f64, vp])
+    _d(lib, "bdx_rt_overlap_probe", [vp, i64, vp, i32, vp])
     _d(lib, "bdx_rt_bind_x", [vp, vp])
     _d(lib, "bdx_rt_wait", [vp])
     _d(lib, "bdx_rt_profile", [vp, ctypes.c_long, vp, i32])

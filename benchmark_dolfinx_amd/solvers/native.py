@@ -163,6 +163,45 @@ class NativeCGRuntime:
         self.tiled = bool(self.lib.bdx_rt_tiled(self.h))
         self.graphs = False
 
+    def comm_priority(self) -> dict:
+        """Priority of the comm stream and the device's range (HIP: a lower
+        value is a higher priority)."""
+        out = (ctypes.c_int * 3)()
+        _check(self.lib.bdx_rt_comm_priority(self.h, out), "rt_comm_priority")
+        return {"least": out[0], "greatest": out[1], "comm_stream": out[2]}
+
+    def preflight(self, timeout_s: float = 60.0) -> dict:
+        """One forward halo exchange and a device all-reduce of (rank + 1),
+        bounded by `timeout_s`: raises if a peer never joins or the sum is
+        wrong (every rank must call it)."""
+        out = (ctypes.c_double * 2)()
+        _check(self.lib.bdx_rt_preflight(self.h, float(timeout_s), out), "rt_preflight")
+        n = self.pb.comm.size
+        want = n * (n + 1) / 2
+        if out[1] != want:
+            raise RuntimeError(f"pre-flight all-reduce returned {out[1]}, expected {want}")
+        return {"ms": float(out[0]), "allreduce": float(out[1])}
+
+    def overlap_probe(self, n: int, reps: int = 5) -> dict:
+        """One-rank probe of the split schedule (runtime.hip overlap_probe):
+        an RCCL self send/recv of n doubles, the boundary tiles and a second
+        send/recv on the comm stream under the interior tiles.  Clobbers the
+        CG state (restart CG afterwards)."""
+        buf = torch.zeros(2 * int(n), dtype=torch.float64, device=self.pb.device)
+        buf[:n] = torch.arange(n, dtype=torch.float64, device=self.pb.device)
+        out = (ctypes.c_double * 5)()
+        torch.cuda.synchronize()
+        _check(self.lib.bdx_rt_overlap_probe(self.h, int(n), ptr(buf), int(reps), out),
+               "rt_overlap_probe")
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(buf[n:], buf[:n]))
+        keys = ("chain_alone_ms", "interior_alone_ms", "chain_done_ms", "interior_done_ms",
+                "exchange_alone_ms")
+        rec = {k: float(v) for k, v in zip(keys, out)}
+        rec["exchange_ok"] = ok
+        rec["bytes"] = int(n) * 8
+        return rec
+
     def comm_ranks(self) -> int:
         """Ranks of the runtime's own communicator (ncclCommCount for RCCL)."""
         return int(self.lib.bdx_rt_comm_count(self.h))

@@ -48,7 +48,12 @@ def test_self_launch_four_ranks_matches_one_rank():
             assert comp["steps"] == 3 and comp["warmup"] == 1 and comp["degree"] == 6
             assert comp["dtype"] == ("fp64" if c == "q6" else "fp32")
             assert rec[f"{c}_gdofs"] == comp["value"] > 0
-    for c, tol in (("q6", 1e-12), ("q6f32", 1e-4)):
+        # the north star's random coefficients, on the headline's own clock
+        rk = rec["companions"]["random_kappa"]
+        assert rk.get("error") is None and rk["kappa"] == "random" and rk["steps"] == 3
+        assert rk["degree"] == 3 and rk["mesh"] == rec["config"]["mesh"]
+        assert rec["random_kappa_gdofs"] == rk["value"] > 0
+    for c, tol in (("q6", 1e-12), ("q6f32", 1e-4), ("random_kappa", 1e-12)):
         a, b = one["companions"][c]["y_norm"], four["companions"][c]["y_norm"]
         assert abs(a - b) <= tol * abs(a), (c, a, b)
     assert one["n_gpus"] == 1 and four["n_gpus"] == 4
@@ -86,10 +91,29 @@ def test_self_launch_kills_siblings_when_a_rank_fails():
                timeout=240, BDX_BENCH_FAIL_RANK="2")
     assert r.returncode != 0
     assert "stopping the other ranks" in r.stderr
-    assert not [s for s in r.stdout.splitlines() if s.startswith("{")]
+    # one JSON line, from the launcher: no value, the error
+    lines = [s for s in r.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] is None and "exited with" in rec["error"]
     # ranks 0/1 would wait for rank 2 in the rendezvous forever; the launcher
     # must end them well before torch's own 600 s timeout
     assert time.time() - t0 < 200
+
+
+def test_failed_companion_on_several_ranks_reports_headline_and_error():
+    """A secondary measurement that fails on a multi-rank run is fatal (a rank
+    that skipped ahead would pair up the wrong collectives), but rank 0 still
+    prints one JSON line: the headline it measured and the error."""
+    r = _bench(["--gpus", "2", "--dofs-per-gpu", "6000", "--steps", "2", "--warmup", "1",
+                "--profile-steps", "0"], timeout=300, BDX_BENCH_FAIL_MEASURE="q6f32")
+    assert r.returncode != 0
+    lines = [s for s in r.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert "injected failure in the q6f32" in rec["error"]
+    assert rec["value"] > 0 and rec["n_gpus"] == 2          # the headline survived
+    assert rec["q6_gdofs"] > 0 and rec["q6f32_gdofs"] is None
 
 
 def test_world_size_mismatch_is_refused():

@@ -1,0 +1,87 @@
+"""Does the split schedule's comm chain get CUs under a full interior launch?
+
+At N > 1 the native runtime (csrc/hip/runtime.hip, CGRuntime::step) forks
+the comm stream off the compute stream: forward halo send/recv -> the last
+tile row and column (the tiles that read ghost planes) -> reverse send/recv,
+while the compute stream runs one launch over every interior tile.  The
+reference overlaps the same way (src/laplacian.hpp:281-349: scatter_fwd_begin,
+interior cells, scatter_fwd_end, boundary cells).  The overlap only holds if
+RCCL's kernels and the boundary launches are dispatched while the interior
+grid still occupies the chip.
+
+RCCL refuses two ranks on one GPU, so this replays the chain of a rank with y
+and z ghost planes (the 1 x 2 x 4 split of N = 8) on a 1-rank RCCL
+communicator: grouped self send/recv of that rank's halo volume at N = 8 (the
+largest exchange of any of the 8 ranks at the weak-scaled mesh), the boundary
+tiles, a second send/recv -- on the runtime's comm stream (greatest device
+priority) -- concurrently with the interior tile rectangle of the same
+300 M / 500 M DoF operator on the compute stream.  The chain must complete
+before the interior launch does.  BDX_PROBE_OUT=<file> appends the record.
+"""
+
+import json
+import os
+
+import pytest
+import torch
+
+from benchmark_dolfinx_amd.driver import make_operator
+from benchmark_dolfinx_amd.fem.mesh import compute_mesh_size, make_local_lattice
+from benchmark_dolfinx_amd.models.poisson import PoissonProblem
+from benchmark_dolfinx_amd.parallel.comm import Comm
+from benchmark_dolfinx_amd.solvers.cg import DeviceCG
+
+
+def halo_elems_at(nranks: int, degree: int, dofs_per_gpu: int) -> int:
+    """Largest one-way halo (elements) of any rank of the weak-scaled N-rank
+    run, on the GPU partition (x kept whole)."""
+    nx = compute_mesh_size(dofs_per_gpu * nranks, degree)
+    best = 0
+    for r in range(nranks):
+        lat = make_local_lattice(r, nranks, nx, degree, whole_x=True)
+        send = sum(b.size for b in lat.halo_send_boxes())
+        recv = sum(b.size for b in lat.halo_recv_boxes())
+        best = max(best, send, recv)
+    return best
+
+
+def test_halo_volume_at_8_ranks_is_plane_sized():
+    n = halo_elems_at(8, 3, 300_000_000)
+    # 1 x 2 x 4 split of the (441, 446, 451) Q3 mesh: one y plane + one z
+    # plane of a 1324 x 669 x 338 block, ~1.3 M DoFs (10.7 MB in FP64)
+    assert 1_000_000 < n < 1_600_000, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("degree,dofs", [(3, 300_000_000), (6, 500_000_000)])
+def test_comm_chain_completes_under_interior_launch(degree, dofs):
+    torch.cuda.set_device(0)
+    nelem = halo_elems_at(8, degree, dofs)
+    pb = PoissonProblem(Comm(), compute_mesh_size(dofs, degree), degree, 1, False,
+                        torch.float64, "gpu")
+    u = pb.assemble_rhs()
+    x = pb.new_vector()
+    op = make_operator(pb, "auto", "auto")
+    cg = DeviceCG(pb)
+    cg.start(op, x, u)
+    rt = op._rt
+    assert rt is not None, "native runtime not loaded"
+    prio = rt.comm_priority()
+    rec = rt.overlap_probe(nelem, reps=5)
+    rec.update(config=f"Q{degree} {pb.ndofs_global} DoFs fp64", kernel=op.name,
+               nty=op.nty, ntz=op.ntz, nseg=op.nseg, priority=prio)
+    print(json.dumps(rec))
+    out = os.environ.get("BDX_PROBE_OUT")
+    if out:
+        with open(out, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    op.close()
+    del op, cg, x, u, pb
+    torch.cuda.empty_cache()
+    assert rec["exchange_ok"], "RCCL self send/recv moved the wrong data"
+    assert prio["comm_stream"] == prio["greatest"]
+    # the whole chain (2 exchanges of the N = 8 halo + the boundary tiles)
+    # must land before the interior tiles finish
+    assert rec["chain_done_ms"] < rec["interior_done_ms"], rec
+    # and the interior must not be slowed much by sharing the chip with it
+    assert rec["interior_done_ms"] < 1.25 * (rec["interior_alone_ms"] + rec["chain_alone_ms"]), rec
