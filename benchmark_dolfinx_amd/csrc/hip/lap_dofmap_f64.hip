@@ -23,3 +23,21 @@ extern "C" int bdx_dofmap_mark_writers(const int* cells_a, int na, const int* ce
   if (nb > 0) dofmap_mark_kernel<<<grid(nb), 256, 0, st>>>(cells_b, nb, cdofs, nd3, pos_b, first);
   return static_cast<int>(hipGetLastError());
 }
+
+// p.Ap partials (blocks) of a CG launch over ncl cells at this rule (the
+// native runtime places the boundary launch's partials after the interior's)
+extern "C" int bdx_dofmap_nblocks(int nq, int ncl) {
+  int cpb = 0;
+  if (ncl <= 0) return 0;
+  switch (nq) {
+    case 2: return dofmap_blocks<2>(ncl, &cpb);
+    case 3: return dofmap_blocks<3>(ncl, &cpb);
+    case 4: return dofmap_blocks<4>(ncl, &cpb);
+    case 5: return dofmap_blocks<5>(ncl, &cpb);
+    case 6: return dofmap_blocks<6>(ncl, &cpb);
+    case 7: return dofmap_blocks<7>(ncl, &cpb);
+    case 8: return dofmap_blocks<8>(ncl, &cpb);
+    case 9: return dofmap_blocks<9>(ncl, &cpb);
+  }
+  return -1;
+}

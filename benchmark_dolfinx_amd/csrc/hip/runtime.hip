@@ -49,6 +49,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "bdx_common.h"
@@ -116,6 +117,23 @@ BDX_DECL_APPLY(4, double, f64, 3)
   BDX_DECL_APPLY(5, T, SUF, 6) BDX_DECL_APPLY(5, T, SUF, 7)
 BDX_DECL_F5(double, f64)
 BDX_DECL_F5(float, f32)
+
+// The dofmap data model's entry points (lap_dofmap.h, lap_dofmap_f{32,64}.hip).
+#define BDX_DECL_DOF(T, SUF)                                                                  \
+  extern "C" int bdx_dofmap_apply_##SUF(                                                      \
+      int, int, int, int, const T*, const int*, int, int64_t, const int*, const int*, const T*, \
+      const unsigned char*, const T*, double, const T*, const T*, const T*, T*, T*, T*,        \
+      const double*, int, int, int, int, double*, int*, hipStream_t);                          \
+  extern "C" int bdx_dofmap_cg_update_##SUF(int64_t, const unsigned char*, T*, T*,              \
+                                            const double*, int, int, double*, int*, hipStream_t); \
+  extern "C" int bdx_dofmap_xflush_##SUF(int64_t, T*, const T*, const double*, int, int,        \
+                                         hipStream_t);
+BDX_DECL_DOF(double, f64)
+BDX_DECL_DOF(float, f32)
+// p.Ap partials of a dofmap launch (lap_dofmap_f64.hip)
+extern "C" int bdx_dofmap_nblocks(int nq, int ncl);
+// capacity of the partials buffers (blas.hip)
+extern "C" int bdx_hip_partials_size();
 
 namespace {
 
@@ -394,8 +412,8 @@ enum Mark {
   kMStart = 0,   // compute stream: iteration start
   kMFwdBeg,      // comm stream: forward exchange start
   kMFwdEnd,      // comm stream: ghost planes of r unpacked
-  kMOpA,         // compute: interior tiles done (serial: the whole operator)
-  kMBnd,         // comm: ghost-touching tiles + ghost finalize done
+  kMOpA,         // compute: interior tiles / cells done (serial: the whole operator)
+  kMBnd,         // comm: ghost-touching tiles / cells (+ ghost finalize) done
   kMRevBeg,      // comm: reverse exchange start
   kMRevEnd,      // comm: reverse send done (serial: + unpack-add)
   kMJoin,        // compute: comm stream joined, received sums added
@@ -405,20 +423,14 @@ enum Mark {
   kNMarks
 };
 
-struct RtConfig {
-  int64_t latd[21];
-  int64_t latdT[21];  // tiled-storage descriptor (tsy = 0: lattice layout)
-  int64_t own[3];
-  int version, affine, P, nq, nblocks, nty, ntz, sy, sz, nseg;
-  double kappa;
-  std::vector<double> wts, qpts;
-};
-
-template <typename T>
-struct CGRuntime {
-  RtConfig cfg;
+// What the fused-structured and the dofmap CG runtimes share: the transport,
+// the two streams, the plane halo, the batched / watchdog-bounded iteration
+// loop with its graph capture, the phase profiler and the pre-flight.  A
+// derived runtime supplies one iteration (`step`) and the final x flush.
+struct LoopBase {
   std::unique_ptr<Transport> tr;
   int nranks = 1, rank = 0;
+  int esize = 8;  // vector element bytes
   // comm stream priority (hipDeviceGetStreamPriorityRange: least, greatest;
   // the priority cs was created with)
   int prio_least = 0, prio_greatest = 0, prio_cs = 0;
@@ -428,31 +440,15 @@ struct CGRuntime {
   // `ext` with events at the start and end of every iterate()
   hipStream_t st = nullptr, cs = nullptr, ext = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_rev = nullptr;
-  ApplyFn<T> apply = nullptr;
-  std::vector<T> tabs_host;
-  const T* tabs = nullptr;  // host copy (fused2-4: kernarg tables) or device buffer (fused5)
-  T *x, *r, *pa, *pb, *y, *yb, *zb, *cb;
-  // Tiled storage (cfg.latdT[17] != 0): the iteration runs on tiled copies
-  // xt, rt, pat, pbt, yt (allocated zeroed by the caller: the padding stays
-  // zero); r and x are imported after each prologue and x is exported after
-  // every iterate() / profile().  wx .. wy: the buffers the loop works on.
-  bool tiled = false, need_import = false;
-  T *xt = nullptr, *rt_ = nullptr, *pat = nullptr, *pbt = nullptr, *yt = nullptr;
-  T *wx, *wr, *wpa, *wpb, *wy;
+  // halo: owned lower faces <-> ghost planes (parallel/halo.py layout), on
+  // the storage layout `wlatd` describes
+  bool halo = false, split = false;
   const int64_t* wlatd = nullptr;
-  const T* xv;
-  const T* kc = nullptr;
-  double *scal, *partials, *upart;
-  // halo: owned lower faces <-> ghost planes (parallel/halo.py layout)
-  bool halo = false;
-  T *hbuf_a = nullptr, *hbuf_b = nullptr;
+  void *hbuf_a = nullptr, *hbuf_b = nullptr;
   const int64_t *face_boxes = nullptr, *ghost_boxes = nullptr;
   int nface_boxes = 0, nghost_boxes = 0;
   int64_t face_total = 0, ghost_total = 0;
   std::vector<int64_t> face_cnt, face_off, ghost_cnt, ghost_off;
-  // overlapped schedule: tile rectangles {ty0, ty1, tz0, tz1}
-  bool split = false;
-  int rect_a[4], rect_r1[4], rect_r2[4];  // interior, last tile row, last tile column
   // phase profiling (eager iterations only)
   bool prof = false;
   hipEvent_t pev[kNMarks] = {};
@@ -472,56 +468,124 @@ struct CGRuntime {
   hipEvent_t ev_batch[2] = {nullptr, nullptr};  // in-flight bound (iterate_on_stream)
   std::vector<hipEvent_t> tev;                  // per-step timing events
 
+  virtual ~LoopBase() {
+    drop_graphs();
+    for (auto& e : pev)
+      if (e) hipEventDestroy(e);
+    for (hipEvent_t e : tev) hipEventDestroy(e);
+    for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_rev, ev_batch[0], ev_batch[1]})
+      if (e) hipEventDestroy(e);
+    if (st) hipStreamDestroy(st);
+    if (cs) hipStreamDestroy(cs);
+    if (pf_scal) hipFree(pf_scal);
+  }
+  // One CG iteration with explicit parity / flags (stream-ordered, no sync).
+  // xm: kXSingle (pend 0: no x term; else alpha_prev p_old), kXSave, kXPair.
+  virtual int step(long k, bool first, bool xlag, int xm) = 0;
+  // x += the pending lagged terms (end of iterate() / profile())
+  virtual int flush() = 0;
+  // bring the prologue's state into the loop's own storage (tiled layouts)
+  virtual int import_state() { return 0; }
+  // the vector the forward halo carries (the pre-flight exchanges it)
+  virtual void* halo_vector() = 0;
+  virtual bool tiled() const { return false; }
+
   void mark(int id, hipStream_t s) {
     if (prof) (void)hipEventRecord(pev[id], s);
   }
-  int box_copy(int mode, T* vec, const int64_t* boxes, int nb, int64_t total, T* buf,
+
+  // Streams, events, halo tables and the transport (every runtime kind).
+  // ptrs: hbuf_a, hbuf_b, face_boxes, ghost_boxes.
+  int init_common(hipStream_t ext_stream, void* const* hptrs, const int64_t* halo_sizes,
+                  const int64_t* fcnt, const int64_t* gcnt, int transport, int n, int r,
+                  int64_t group_id) {
+    nranks = n;
+    rank = r;
+    ext = ext_stream;
+    // The comm stream runs at the greatest priority the device offers: its
+    // chain (RCCL send/recv kernels, the boundary work, the reverse send) is
+    // dispatched ahead of the interior launch's queued workgroups as soon as
+    // resident ones retire, instead of after the whole interior grid.
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) {
+      (void)hipGetLastError();
+      prio_least = prio_greatest = 0;
+    }
+    BDX_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    BDX_CHECK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, prio_greatest));
+    BDX_CHECK(hipStreamGetPriority(cs, &prio_cs));
+    for (hipEvent_t* e : {&ev_in, &ev_out, &ev_fork, &ev_rev, &ev_batch[0], &ev_batch[1]})
+      BDX_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    hbuf_a = hptrs[0];
+    hbuf_b = hptrs[1];
+    face_boxes = static_cast<const int64_t*>(hptrs[2]);
+    ghost_boxes = static_cast<const int64_t*>(hptrs[3]);
+    nface_boxes = static_cast<int>(halo_sizes[0]);
+    face_total = halo_sizes[1];
+    nghost_boxes = static_cast<int>(halo_sizes[2]);
+    ghost_total = halo_sizes[3];
+    face_cnt.assign(fcnt, fcnt + n);
+    ghost_cnt.assign(gcnt, gcnt + n);
+    face_off.assign(n, 0);
+    ghost_off.assign(n, 0);
+    for (int p = 1; p < n; ++p) {
+      face_off[p] = face_off[p - 1] + face_cnt[p - 1];
+      ghost_off[p] = ghost_off[p - 1] + ghost_cnt[p - 1];
+    }
+    halo = n > 1 && (face_total + ghost_total) > 0;
+    if (transport == 1 && n > 1) {  // RCCL: connected by bdx_rt_connect
+      auto t = std::make_unique<RcclTransport>();
+      t->nranks = n;
+      tr = std::move(t);
+    } else if (transport == 2 && n > 1) {  // in-process threads
+      auto t = std::make_unique<ThreadTransport>();
+      {
+        std::lock_guard<std::mutex> lk(g_groups_m);
+        auto& g = g_groups[group_id];
+        if (!g) {
+          g = std::make_shared<ThreadGroupState>();
+          g->size = n;
+          g->sbuf.assign(n, nullptr);
+          g->soff.assign(n, nullptr);
+          g->packed.assign(n, nullptr);
+          g->copied.assign(n, nullptr);
+          g->red.assign(n, nullptr);
+        }
+        t->g = g;
+      }
+      t->rank = r;
+      tr = std::move(t);
+    } else {  // single rank: no communication
+      tr = std::make_unique<NoTransport>();
+      halo = false;
+    }
+    return 0;
+  }
+
+  int box_copy(int mode, void* vec, const int64_t* boxes, int nb, int64_t total, void* buf,
                hipStream_t s) {
-    if constexpr (sizeof(T) == 8)
-      return bdx_box_copy_lat_f64(mode, vec, wlatd, boxes, nb, total, buf, s);
-    else
-      return bdx_box_copy_lat_f32(mode, vec, wlatd, boxes, nb, total, buf, s);
-  }
-  int convert(int dir, T* lat, T* til, hipStream_t s) {
-    if constexpr (sizeof(T) == 8)
-      return bdx_layout_convert_f64(dir, cfg.latdT, lat, til, s);
-    else
-      return bdx_layout_convert_f32(dir, cfg.latdT, lat, til, s);
-  }
-  // tiled: bring the prologue's r and x into the tiled copies, p_old = 0
-  int import_state() {
-    if (!tiled || !need_import) return 0;
-    need_import = false;
-    int rc;
-    if ((rc = convert(0, r, rt_, st)) || (rc = convert(0, x, xt, st))) return rc;
-    const BdxLattice L = BdxLattice::from(cfg.latdT);
-    return static_cast<int>(hipMemsetAsync(pat, 0, L.size() * sizeof(T), st));
+    if (esize == 8)
+      return bdx_box_copy_lat_f64(mode, static_cast<double*>(vec), wlatd, boxes, nb, total,
+                                  static_cast<double*>(buf), s);
+    return bdx_box_copy_lat_f32(mode, static_cast<float*>(vec), wlatd, boxes, nb, total,
+                                static_cast<float*>(buf), s);
   }
   // forward: owned lower faces of v -> peers' ghost planes (pack, exchange, unpack)
-  int halo_forward(T* v, hipStream_t s) {
+  int halo_forward(void* v, hipStream_t s) {
     int rc = box_copy(0, v, face_boxes, nface_boxes, face_total, hbuf_a, s);
     if (rc || (rc = tr->exchange(hbuf_a, face_cnt, face_off, hbuf_b, ghost_cnt, ghost_off,
-                                 sizeof(T), s)))
+                                 esize, s)))
       return rc;
     return box_copy(1, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_b, s);
   }
   // reverse, first half: ghost-plane partial sums of v -> peers (pack, exchange)
-  int halo_reverse_send(T* v, hipStream_t s) {
+  int halo_reverse_send(void* v, hipStream_t s) {
     const int rc = box_copy(0, v, ghost_boxes, nghost_boxes, ghost_total, hbuf_a, s);
     if (rc) return rc;
-    return tr->exchange(hbuf_a, ghost_cnt, ghost_off, hbuf_b, face_cnt, face_off, sizeof(T), s);
+    return tr->exchange(hbuf_a, ghost_cnt, ghost_off, hbuf_b, face_cnt, face_off, esize, s);
   }
   // reverse, second half: add the received sums into the owned lower faces
-  int halo_reverse_add(T* v, hipStream_t s) {
+  int halo_reverse_add(void* v, hipStream_t s) {
     return box_copy(2, v, face_boxes, nface_boxes, face_total, hbuf_b, s);
-  }
-  int finalize_ghost(hipStream_t s) {
-    if constexpr (sizeof(T) == 8)
-      return bdx_fused_finalize_f64(wlatd, wy, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
-                                    s);
-    else
-      return bdx_fused_finalize_f32(wlatd, wy, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
-                                    s);
   }
 
   // x mode of the next iteration (kXSingle with pend == 0: no x update)
@@ -530,96 +594,6 @@ struct CGRuntime {
     return pend == 1 ? kXSave : kXPair;
   }
   void advance_pend(int xm) { pend = (pend == 0 || xm == kXPair) ? 1 : (xm == kXSave ? 2 : 1); }
-
-  // The fused operator of iteration k on the tile rectangle `rect` (null:
-  // every tile) on stream s.
-  int launch_op(long k, bool first, bool xlag, int xm, const int* rect, hipStream_t s) {
-    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
-    T* pold = (k % 2 == 0) ? wpa : wpb;
-    T* pnew = (k % 2 == 0) ? wpb : wpa;
-    return apply(1 | (xm << 4) | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(),
-                 cfg.qpts.data(), wr, pold, pnew, wx, wy, yb, zb, cb, xv, kc, tabs, cfg.kappa,
-                 scal, partials, first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
-                 xlag ? kPAP : -1, cfg.nty, cfg.ntz, rect, s);
-  }
-
-  // One CG iteration with explicit parity / flags (stream-ordered, no sync).
-  // xm: kXSingle (pend 0: no x term; else alpha_prev p_old), kXSave, kXPair.
-  int step(long k, bool first, bool xlag, int xm) {
-    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
-    T* const r = wr;
-    T* const y = wy;
-    auto op = [&](const int* rect, hipStream_t s) {
-      return launch_op(k, first, xlag, xm, rect, s);
-    };
-    int rc;
-    mark(kMStart, st);
-    if (split) {
-      // Two streams (reference src/laplacian.hpp:281-349, redesigned):
-      //   cs: forward exchange -> boundary tiles (the last tile row and
-      //       column, which read the ghost planes) -> ghost-plane fold ->
-      //       reverse send;
-      //   st: every interior tile, concurrently -- the exchanges and the
-      //       small boundary launches all ride under the interior launch, so
-      //       none of them is on the critical path as long as the interior
-      //       work outlasts them;
-      //   st: wait for cs, add the received sums into the owned faces.
-      // Write sets are disjoint: a tile writes only its own nodes and its own
-      // interface partials, and the ghost-plane fold reads only partials of
-      // boundary tiles (fused_finalize_ghost_kernel).
-      BDX_CHECK(hipEventRecord(ev_fork, st));
-      BDX_CHECK(hipStreamWaitEvent(cs, ev_fork, 0));
-      mark(kMFwdBeg, cs);
-      if ((rc = halo_forward(r, cs))) return rc;
-      mark(kMFwdEnd, cs);
-      if ((rc = op(rect_r1, cs)) || (rc = op(rect_r2, cs)) || (rc = finalize_ghost(cs)))
-        return rc;
-      mark(kMBnd, cs);
-      mark(kMRevBeg, cs);
-      if ((rc = halo_reverse_send(y, cs))) return rc;
-      BDX_CHECK(hipEventRecord(ev_rev, cs));
-      mark(kMRevEnd, cs);
-      if ((rc = op(rect_a, st))) return rc;
-      mark(kMOpA, st);
-      BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
-      if ((rc = halo_reverse_add(y, st))) return rc;
-      mark(kMJoin, st);
-    } else {
-      mark(kMFwdBeg, st);
-      if (halo && (rc = halo_forward(r, st))) return rc;
-      mark(kMFwdEnd, st);
-      if ((rc = op(nullptr, st))) return rc;
-      mark(kMOpA, st);
-      if (halo && (rc = finalize_ghost(st))) return rc;
-      mark(kMBnd, st);
-      mark(kMRevBeg, st);
-      if (halo && ((rc = halo_reverse_send(y, st)) || (rc = halo_reverse_add(y, st)))) return rc;
-      mark(kMRevEnd, st);
-      mark(kMJoin, st);
-    }
-    if ((rc = bdx_reduce_partials(partials, cfg.nblocks, scal, kPAP, st))) return rc;
-    if (nranks > 1 && (rc = tr->allreduce_sum(scal + kPAP, 1, st))) return rc;
-    mark(kMPap, st);
-    if (tiled) {
-      if constexpr (sizeof(T) == 8)
-        rc = bdx_cg_update_tiled_f64(wlatd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, scal, cur,
-                                     kPAP, nxt, upart, st);
-      else
-        rc = bdx_cg_update_tiled_f32(wlatd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, scal, cur,
-                                     kPAP, nxt, upart, st);
-    } else if constexpr (sizeof(T) == 8) {
-      rc = bdx_cg_update_iface_f64(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
-                                   cfg.sz, scal, cur, kPAP, nxt, upart, st);
-    } else {
-      rc = bdx_cg_update_iface_f32(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
-                                   cfg.sz, scal, cur, kPAP, nxt, upart, st);
-    }
-    if (rc) return rc;
-    mark(kMUpd, st);
-    if (nranks > 1 && (rc = tr->allreduce_sum(scal + nxt, 1, st))) return rc;
-    mark(kMEnd, st);
-    return 0;
-  }
 
   // Capture the steady-state iteration of a parity and x mode (it > 0,
   // lagged x update pending); graph index = parity + 2 * (xm == kXPair).
@@ -716,37 +690,9 @@ struct CGRuntime {
     return flush();
   }
 
-  // x += alpha_last p_last (and, with two terms pending, the saved
-  // alpha_prev p_prev, which is the last iteration's p_old)
-  int flush() {
-    if (pend == 0) return 0;
-    const int last = ((it - 1) % 2 == 0) ? kRR0 : kRR1;
-    T* plast = ((it - 1) % 2 == 0) ? wpb : wpa;  // p_new of the last iteration
-    T* pprev = ((it - 1) % 2 == 0) ? wpa : wpb;  // its p_old
-    const bool two = pend == 2;
-    pend = 0;
-    if (tiled) {  // fold the terms and export x in one pass
-      const T* p2 = two ? pprev : nullptr;
-      if constexpr (sizeof(T) == 8)
-        return bdx_flush_export_f64(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
-                                    -1, st);
-      else
-        return bdx_flush_export_f32(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
-                                    -1, st);
-    }
-    auto one = [&](T* p, int num, int den) {
-      if constexpr (sizeof(T) == 8)
-        return bdx_xflush_f64(cfg.latd, cfg.own, x, p, scal, num, den, st);
-      else
-        return bdx_xflush_f32(cfg.latd, cfg.own, x, p, scal, num, den, st);
-    };
-    int rc = one(plast, last, kPAP);
-    if (!rc && two) rc = one(pprev, kScalXSave, -1);
-    return rc;
-  }
-
   // n eager iterations with timing events between the phases; out[i] = mean
   // ms of interval i (see bdx_rt_profile for the list).
+  static constexpr int kNPhases = 13;
   int profile(long n, double* out, int nout) {
     if (nout < kNPhases) return static_cast<int>(hipErrorInvalidValue);
     for (int i = 0; i < kNMarks; ++i)
@@ -779,8 +725,8 @@ struct CGRuntime {
       };
       out[0] += dt(kMFwdBeg, kMFwdEnd);
       out[1] += dt(kMStart, kMOpA);
-      // split: forward-halo end -> boundary tiles + ghost fold; serial: the
-      // ghost fold only (kMFwdEnd precedes the whole operator there)
+      // split: forward-halo end -> boundary work; serial: the boundary work
+      // only (kMFwdEnd precedes the whole operator there)
       out[2] += split ? dt(kMFwdEnd, kMBnd) : dt(kMOpA, kMBnd);
       out[3] += dt(kMRevBeg, kMRevEnd);
       out[4] += dt(kMOpA, kMJoin);
@@ -789,7 +735,7 @@ struct CGRuntime {
       out[7] += dt(kMUpd, kMEnd);
       out[8] += dt(kMStart, kMEnd);
       // timeline offsets from the iteration start: the comm-stream chain is
-      // hidden when it completes before the interior tiles do
+      // hidden when it completes before the interior work does
       out[9] += dt(kMStart, kMFwdEnd);
       out[10] += dt(kMStart, kMBnd);
       out[11] += dt(kMStart, kMRevEnd);
@@ -802,14 +748,14 @@ struct CGRuntime {
     for (int i = 0; i < kNPhases && n > 0; ++i) out[i] /= static_cast<double>(n);
     return rc;
   }
-  static constexpr int kNPhases = 13;
 
   // Pre-flight of the transport before any timed work (bench.py at N > 1):
-  // one forward halo exchange of r and a device all-reduce of (rank + 1),
-  // under a deadline of timeout_s instead of the run's.  out[0] = host ms
-  // of both, out[1] = the all-reduce result (n (n + 1) / 2 when every rank
-  // took part).  A peer that never joins aborts the communicator: the error
-  // comes back here instead of a hang inside the warmup.
+  // one forward halo exchange of the loop's halo vector and a device
+  // all-reduce of (rank + 1), under a deadline of timeout_s instead of the
+  // run's.  out[0] = host ms of both, out[1] = the all-reduce result
+  // (n (n + 1) / 2 when every rank took part).  A peer that never joins
+  // aborts the communicator: the error comes back here instead of a hang
+  // inside the warmup.
   int preflight(double timeout_s, double* out) {
     if (!pf_scal) BDX_CHECK(hipMalloc(&pf_scal, sizeof(double)));
     const double v = rank + 1.0;
@@ -830,7 +776,7 @@ struct CGRuntime {
     {
       bdx::Watchdog::Busy busy(wd);
       BDX_CHECK(hipMemcpyAsync(pf_scal, &v, sizeof(double), hipMemcpyHostToDevice, st));
-      if (halo) rc = halo_forward(wr, st);
+      if (halo) rc = halo_forward(halo_vector(), st);
       if (!rc && nranks > 1) rc = tr->allreduce_sum(pf_scal, 1, st);
       if (!rc) rc = static_cast<int>(hipEventRecord(ev_out, st));
     }
@@ -840,6 +786,181 @@ struct CGRuntime {
     BDX_CHECK(hipMemcpy(&out[1], pf_scal, sizeof(double), hipMemcpyDeviceToHost));
     BDX_CHECK(hipStreamWaitEvent(ext, ev_out, 0));
     return 0;
+  }
+};
+
+// ---------------------------------------------------- fused structured operator
+struct RtConfig {
+  int64_t latd[21];
+  int64_t latdT[21];  // tiled-storage descriptor (tsy = 0: lattice layout)
+  int64_t own[3];
+  int version, affine, P, nq, nblocks, nty, ntz, sy, sz, nseg;
+  double kappa;
+  std::vector<double> wts, qpts;
+};
+
+template <typename T>
+struct CGRuntime final : LoopBase {
+  RtConfig cfg;
+  ApplyFn<T> apply = nullptr;
+  std::vector<T> tabs_host;
+  const T* tabs = nullptr;  // host copy (fused2-4: kernarg tables) or device buffer (fused5)
+  T *x, *r, *pa, *pb, *y, *yb, *zb, *cb;
+  // Tiled storage (cfg.latdT[17] != 0): the iteration runs on tiled copies
+  // xt, rt, pat, pbt, yt (allocated zeroed by the caller: the padding stays
+  // zero); r and x are imported after each prologue and x is exported after
+  // every iterate() / profile().  wx .. wy: the buffers the loop works on.
+  bool is_tiled = false, need_import = false;
+  T *xt = nullptr, *rt_ = nullptr, *pat = nullptr, *pbt = nullptr, *yt = nullptr;
+  T *wx, *wr, *wpa, *wpb, *wy;
+  const T* xv;
+  const T* kc = nullptr;
+  double *scal, *partials, *upart;
+  // overlapped schedule: tile rectangles {ty0, ty1, tz0, tz1}
+  int rect_a[4], rect_r1[4], rect_r2[4];  // interior, last tile row, last tile column
+
+  bool tiled() const override { return is_tiled; }
+  void* halo_vector() override { return wr; }
+
+  int convert(int dir, T* lat, T* til, hipStream_t s) {
+    if constexpr (sizeof(T) == 8)
+      return bdx_layout_convert_f64(dir, cfg.latdT, lat, til, s);
+    else
+      return bdx_layout_convert_f32(dir, cfg.latdT, lat, til, s);
+  }
+  // tiled: bring the prologue's r and x into the tiled copies, p_old = 0
+  int import_state() override {
+    if (!is_tiled || !need_import) return 0;
+    need_import = false;
+    int rc;
+    if ((rc = convert(0, r, rt_, st)) || (rc = convert(0, x, xt, st))) return rc;
+    const BdxLattice L = BdxLattice::from(cfg.latdT);
+    return static_cast<int>(hipMemsetAsync(pat, 0, L.size() * sizeof(T), st));
+  }
+  int finalize_ghost(hipStream_t s) {
+    if constexpr (sizeof(T) == 8)
+      return bdx_fused_finalize_f64(wlatd, wy, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
+                                    s);
+    else
+      return bdx_fused_finalize_f32(wlatd, wy, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy, cfg.sz, 1,
+                                    s);
+  }
+
+  // The fused operator of iteration k on the tile rectangle `rect` (null:
+  // every tile) on stream s.
+  int launch_op(long k, bool first, bool xlag, int xm, const int* rect, hipStream_t s) {
+    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
+    T* pold = (k % 2 == 0) ? wpa : wpb;
+    T* pnew = (k % 2 == 0) ? wpb : wpa;
+    return apply(1 | (xm << 4) | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(),
+                 cfg.qpts.data(), wr, pold, pnew, wx, wy, yb, zb, cb, xv, kc, tabs, cfg.kappa,
+                 scal, partials, first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
+                 xlag ? kPAP : -1, cfg.nty, cfg.ntz, rect, s);
+  }
+
+  int step(long k, bool first, bool xlag, int xm) override {
+    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
+    T* const r = wr;
+    T* const y = wy;
+    auto op = [&](const int* rect, hipStream_t s) {
+      return launch_op(k, first, xlag, xm, rect, s);
+    };
+    int rc;
+    mark(kMStart, st);
+    if (split) {
+      // Two streams (reference src/laplacian.hpp:281-349, redesigned):
+      //   cs: forward exchange -> boundary tiles (the last tile row and
+      //       column, which read the ghost planes) -> ghost-plane fold ->
+      //       reverse send;
+      //   st: every interior tile, concurrently -- the exchanges and the
+      //       small boundary launches all ride under the interior launch, so
+      //       none of them is on the critical path as long as the interior
+      //       work outlasts them;
+      //   st: wait for cs, add the received sums into the owned faces.
+      // Write sets are disjoint: a tile writes only its own nodes and its own
+      // interface partials, and the ghost-plane fold reads only partials of
+      // boundary tiles (fused_finalize_ghost_kernel).
+      BDX_CHECK(hipEventRecord(ev_fork, st));
+      BDX_CHECK(hipStreamWaitEvent(cs, ev_fork, 0));
+      mark(kMFwdBeg, cs);
+      if ((rc = halo_forward(r, cs))) return rc;
+      mark(kMFwdEnd, cs);
+      if ((rc = op(rect_r1, cs)) || (rc = op(rect_r2, cs)) || (rc = finalize_ghost(cs)))
+        return rc;
+      mark(kMBnd, cs);
+      mark(kMRevBeg, cs);
+      if ((rc = halo_reverse_send(y, cs))) return rc;
+      BDX_CHECK(hipEventRecord(ev_rev, cs));
+      mark(kMRevEnd, cs);
+      if ((rc = op(rect_a, st))) return rc;
+      mark(kMOpA, st);
+      BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
+      if ((rc = halo_reverse_add(y, st))) return rc;
+      mark(kMJoin, st);
+    } else {
+      mark(kMFwdBeg, st);
+      if (halo && (rc = halo_forward(r, st))) return rc;
+      mark(kMFwdEnd, st);
+      if ((rc = op(nullptr, st))) return rc;
+      mark(kMOpA, st);
+      if (halo && (rc = finalize_ghost(st))) return rc;
+      mark(kMBnd, st);
+      mark(kMRevBeg, st);
+      if (halo && ((rc = halo_reverse_send(y, st)) || (rc = halo_reverse_add(y, st)))) return rc;
+      mark(kMRevEnd, st);
+      mark(kMJoin, st);
+    }
+    if ((rc = bdx_reduce_partials(partials, cfg.nblocks, scal, kPAP, st))) return rc;
+    if (nranks > 1 && (rc = tr->allreduce_sum(scal + kPAP, 1, st))) return rc;
+    mark(kMPap, st);
+    if (is_tiled) {
+      if constexpr (sizeof(T) == 8)
+        rc = bdx_cg_update_tiled_f64(wlatd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, scal, cur,
+                                     kPAP, nxt, upart, st);
+      else
+        rc = bdx_cg_update_tiled_f32(wlatd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, scal, cur,
+                                     kPAP, nxt, upart, st);
+    } else if constexpr (sizeof(T) == 8) {
+      rc = bdx_cg_update_iface_f64(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
+                                   cfg.sz, scal, cur, kPAP, nxt, upart, st);
+    } else {
+      rc = bdx_cg_update_iface_f32(cfg.latd, cfg.own, r, y, yb, zb, cb, cfg.nty, cfg.ntz, cfg.sy,
+                                   cfg.sz, scal, cur, kPAP, nxt, upart, st);
+    }
+    if (rc) return rc;
+    mark(kMUpd, st);
+    if (nranks > 1 && (rc = tr->allreduce_sum(scal + nxt, 1, st))) return rc;
+    mark(kMEnd, st);
+    return 0;
+  }
+
+  // x += alpha_last p_last (and, with two terms pending, the saved
+  // alpha_prev p_prev, which is the last iteration's p_old)
+  int flush() override {
+    if (pend == 0) return 0;
+    const int last = ((it - 1) % 2 == 0) ? kRR0 : kRR1;
+    T* plast = ((it - 1) % 2 == 0) ? wpb : wpa;  // p_new of the last iteration
+    T* pprev = ((it - 1) % 2 == 0) ? wpa : wpb;  // its p_old
+    const bool two = pend == 2;
+    pend = 0;
+    if (is_tiled) {  // fold the terms and export x in one pass
+      const T* p2 = two ? pprev : nullptr;
+      if constexpr (sizeof(T) == 8)
+        return bdx_flush_export_f64(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
+                                    -1, st);
+      else
+        return bdx_flush_export_f32(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
+                                    -1, st);
+    }
+    auto one = [&](T* p, int num, int den) {
+      if constexpr (sizeof(T) == 8)
+        return bdx_xflush_f64(cfg.latd, cfg.own, x, p, scal, num, den, st);
+      else
+        return bdx_xflush_f32(cfg.latd, cfg.own, x, p, scal, num, den, st);
+    };
+    int rc = one(plast, last, kPAP);
+    if (!rc && two) rc = one(pprev, kScalXSave, -1);
+    return rc;
   }
 
   // Overlap probe (one rank only): does a comm-stream chain get CUs while the
@@ -925,39 +1046,139 @@ struct CGRuntime {
     }
     return 0;
   }
-
-  ~CGRuntime() {
-    drop_graphs();
-    for (auto& e : pev)
-      if (e) hipEventDestroy(e);
-    for (hipEvent_t e : tev) hipEventDestroy(e);
-    for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_rev, ev_batch[0], ev_batch[1]})
-      if (e) hipEventDestroy(e);
-    if (st) hipStreamDestroy(st);
-    if (cs) hipStreamDestroy(cs);
-    if (pf_scal) hipFree(pf_scal);
-  }
 };
 
-struct Handle {
-  int is_f64;
-  void* rt;
+// -------------------------------------------------------------- dofmap operator
+// The reference's data model (explicit cell -> dof map, stored or on-the-fly G,
+// atomic scatter; csrc/hip/lap_dofmap.h) on the same loop: the interior cells
+// run on the compute stream while the comm stream does the forward exchange,
+// the boundary cells (those touching a ghost dof) and the reverse send of the
+// ghost partial sums -- the reference's scatter_fwd_begin / lcells /
+// scatter_fwd_end / bcells schedule (src/laplacian.hpp:281-349), without its
+// host syncs and with the boundary cells off the critical path.
+struct DofConfig {
+  int64_t latd[21];
+  int P, nq, geom, n_inner, n_outer, nb_inner, nb_outer;
+  int64_t nvec;
+  double kappa;
 };
 
 template <typename T>
-Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, double kappa,
-               const double* wts, const double* qpts, const void* tabs, void* const* ptrs,
-               const int64_t* halo_sizes, const int64_t* face_cnt, const int64_t* ghost_cnt,
-               int transport, int nranks, int rank, int64_t group_id, hipStream_t st,
-               const int64_t* latd_tiled, void* const* tptrs) {
+struct DofCGRuntime final : LoopBase {
+  DofConfig cfg;
+  const T* tab = nullptr;
+  const int *inner = nullptr, *outer = nullptr, *cdofs = nullptr, *cverts = nullptr;
+  const T *coords = nullptr, *G = nullptr, *kc = nullptr;
+  const unsigned char* flags = nullptr;
+  T *x, *r, *pa, *pb, *y;
+  double *scal, *partials, *upart;
+
+  void* halo_vector() override { return r; }
+
+  int run(const int* cells, int ncl, double* part, long k, bool first, bool xlag,
+          hipStream_t s) {
+    if (ncl <= 0) return 0;
+    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
+    T* pold = (k % 2 == 0) ? pa : pb;
+    T* pnew = (k % 2 == 0) ? pb : pa;
+    int nb = 0;
+    int rc;
+    if constexpr (sizeof(T) == 8)
+      rc = bdx_dofmap_apply_f64(cfg.P, cfg.nq, cfg.geom, 1, tab, cells, ncl, cfg.nvec, cdofs,
+                                cverts, coords, flags, G, cfg.kappa, kc, r, pold, pnew, x, y, scal,
+                                first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
+                                xlag ? kPAP : -1, part, &nb, s);
+    else
+      rc = bdx_dofmap_apply_f32(cfg.P, cfg.nq, cfg.geom, 1, tab, cells, ncl, cfg.nvec, cdofs,
+                                cverts, coords, flags, G, cfg.kappa, kc, r, pold, pnew, x, y, scal,
+                                first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
+                                xlag ? kPAP : -1, part, &nb, s);
+    return rc;
+  }
+
+  int step(long k, bool first, bool xlag, int /*xm*/) override {
+    const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
+    double* const part_b = partials + cfg.nb_inner;
+    int rc;
+    mark(kMStart, st);
+    if (split) {
+      // cs: forward exchange -> boundary cells -> reverse send of the ghost
+      // partials; st: the interior cells (they touch no ghost dof), then the
+      // received sums are added into the owned faces.  Both kernels add into
+      // y with float atomics and write p / x only at their designated dofs
+      // (lap_dofmap.h writer marks), so they may run concurrently.
+      BDX_CHECK(hipEventRecord(ev_fork, st));
+      BDX_CHECK(hipStreamWaitEvent(cs, ev_fork, 0));
+      mark(kMFwdBeg, cs);
+      if ((rc = halo_forward(r, cs))) return rc;
+      mark(kMFwdEnd, cs);
+      if ((rc = run(outer, cfg.n_outer, part_b, k, first, xlag, cs))) return rc;
+      mark(kMBnd, cs);
+      mark(kMRevBeg, cs);
+      if ((rc = halo_reverse_send(y, cs))) return rc;
+      BDX_CHECK(hipEventRecord(ev_rev, cs));
+      mark(kMRevEnd, cs);
+      if ((rc = run(inner, cfg.n_inner, partials, k, first, xlag, st))) return rc;
+      mark(kMOpA, st);
+      BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
+      if ((rc = halo_reverse_add(y, st))) return rc;
+      mark(kMJoin, st);
+    } else {
+      mark(kMFwdBeg, st);
+      if (halo && (rc = halo_forward(r, st))) return rc;
+      mark(kMFwdEnd, st);
+      if ((rc = run(inner, cfg.n_inner, partials, k, first, xlag, st))) return rc;
+      mark(kMOpA, st);
+      if ((rc = run(outer, cfg.n_outer, part_b, k, first, xlag, st))) return rc;
+      mark(kMBnd, st);
+      mark(kMRevBeg, st);
+      if (halo && ((rc = halo_reverse_send(y, st)) || (rc = halo_reverse_add(y, st)))) return rc;
+      mark(kMRevEnd, st);
+      mark(kMJoin, st);
+    }
+    if ((rc = bdx_reduce_partials(partials, cfg.nb_inner + cfg.nb_outer, scal, kPAP, st)))
+      return rc;
+    if (nranks > 1 && (rc = tr->allreduce_sum(scal + kPAP, 1, st))) return rc;
+    mark(kMPap, st);
+    int nu = 0;
+    if constexpr (sizeof(T) == 8)
+      rc = bdx_dofmap_cg_update_f64(cfg.nvec, flags, r, y, scal, cur, kPAP, upart, &nu, st);
+    else
+      rc = bdx_dofmap_cg_update_f32(cfg.nvec, flags, r, y, scal, cur, kPAP, upart, &nu, st);
+    if (rc || (rc = bdx_reduce_partials(upart, nu, scal, nxt, st))) return rc;
+    mark(kMUpd, st);
+    if (nranks > 1 && (rc = tr->allreduce_sum(scal + nxt, 1, st))) return rc;
+    mark(kMEnd, st);
+    return 0;
+  }
+
+  int flush() override {
+    if (pend == 0) return 0;
+    pend = 0;
+    const int last = ((it - 1) % 2 == 0) ? kRR0 : kRR1;
+    T* plast = ((it - 1) % 2 == 0) ? pb : pa;  // p_new of the last iteration
+    if constexpr (sizeof(T) == 8)
+      return bdx_dofmap_xflush_f64(cfg.nvec, x, plast, scal, last, kPAP, st);
+    else
+      return bdx_dofmap_xflush_f32(cfg.nvec, x, plast, scal, last, kPAP, st);
+  }
+};
+
+// iparams of the fused kind: version, affine, P, nq, nblocks, nty, ntz, sy,
+// sz, use_graph, overlap, nseg (nblocks = nty * ntz * nseg p.Ap partials)
+template <typename T>
+LoopBase* create(const int64_t* latd, const int64_t* own, const int* iparams, double kappa,
+                 const double* wts, const double* qpts, const void* tabs, void* const* ptrs,
+                 const int64_t* halo_sizes, const int64_t* face_cnt, const int64_t* ghost_cnt,
+                 int transport, int nranks, int rank, int64_t group_id, hipStream_t st,
+                 const int64_t* latd_tiled, void* const* tptrs) {
   auto rt = std::make_unique<CGRuntime<T>>();
+  rt->esize = sizeof(T);
   RtConfig& c = rt->cfg;
   std::memcpy(c.latd, latd, sizeof(c.latd));
   std::memset(c.latdT, 0, sizeof(c.latdT));
   if (latd_tiled && latd_tiled[17] && tptrs) std::memcpy(c.latdT, latd_tiled, sizeof(c.latdT));
   std::memcpy(c.own, own, sizeof(c.own));
-  // iparams: version, affine, P, nq, nblocks, nty, ntz, sy, sz, use_graph, overlap, nseg
-  // (nblocks = nty * ntz * nseg p.Ap partials)
   c.version = iparams[0];
   c.affine = iparams[1];
   c.P = iparams[2];
@@ -1001,13 +1222,11 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
   rt->scal = static_cast<double*>(ptrs[i++]);
   rt->partials = static_cast<double*>(ptrs[i++]);
   rt->upart = static_cast<double*>(ptrs[i++]);
-  rt->hbuf_a = static_cast<T*>(ptrs[i++]);
-  rt->hbuf_b = static_cast<T*>(ptrs[i++]);
-  rt->face_boxes = static_cast<const int64_t*>(ptrs[i++]);
-  rt->ghost_boxes = static_cast<const int64_t*>(ptrs[i++]);
+  void* const* hptrs = ptrs + i;  // hbuf_a, hbuf_b, face_boxes, ghost_boxes
+  i += 4;
   rt->kc = static_cast<const T*>(ptrs[i++]);
-  rt->tiled = c.latdT[17] != 0;
-  if (rt->tiled) {
+  rt->is_tiled = c.latdT[17] != 0;
+  if (rt->is_tiled) {
     // only the x-march kernels whose tile is the storage tile address it
     if ((c.version < 3 || c.version > 5) || c.latdT[17] != c.sy || c.latdT[18] != c.sz)
       return nullptr;
@@ -1018,44 +1237,15 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
     rt->yt = static_cast<T*>(tptrs[4]);
     if (!rt->xt || !rt->rt_ || !rt->pat || !rt->pbt || !rt->yt) return nullptr;
   }
-  rt->wx = rt->tiled ? rt->xt : rt->x;
-  rt->wr = rt->tiled ? rt->rt_ : rt->r;
-  rt->wpa = rt->tiled ? rt->pat : rt->pa;
-  rt->wpb = rt->tiled ? rt->pbt : rt->pb;
-  rt->wy = rt->tiled ? rt->yt : rt->y;
-  rt->wlatd = rt->tiled ? c.latdT : c.latd;
-  rt->nface_boxes = static_cast<int>(halo_sizes[0]);
-  rt->face_total = halo_sizes[1];
-  rt->nghost_boxes = static_cast<int>(halo_sizes[2]);
-  rt->ghost_total = halo_sizes[3];
-  rt->nranks = nranks;
-  rt->ext = st;
-  // The comm stream runs at the greatest priority the device offers: its
-  // chain (RCCL send/recv kernels, the boundary tiles, the ghost fold) is
-  // dispatched ahead of the interior launch's queued workgroups as soon as
-  // resident ones retire, instead of after the whole interior grid.
-  if (hipDeviceGetStreamPriorityRange(&rt->prio_least, &rt->prio_greatest) != hipSuccess) {
-    (void)hipGetLastError();
-    rt->prio_least = rt->prio_greatest = 0;
-  }
-  if (hipStreamCreateWithFlags(&rt->st, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithPriority(&rt->cs, hipStreamNonBlocking, rt->prio_greatest) !=
-          hipSuccess ||
-      hipStreamGetPriority(rt->cs, &rt->prio_cs) != hipSuccess)
+  rt->wx = rt->is_tiled ? rt->xt : rt->x;
+  rt->wr = rt->is_tiled ? rt->rt_ : rt->r;
+  rt->wpa = rt->is_tiled ? rt->pat : rt->pa;
+  rt->wpb = rt->is_tiled ? rt->pbt : rt->pb;
+  rt->wy = rt->is_tiled ? rt->yt : rt->y;
+  rt->wlatd = rt->is_tiled ? c.latdT : c.latd;
+  if (rt->init_common(st, hptrs, halo_sizes, face_cnt, ghost_cnt, transport, nranks, rank,
+                      group_id))
     return nullptr;
-  rt->rank = rank;
-  for (hipEvent_t* e : {&rt->ev_in, &rt->ev_out, &rt->ev_fork,
-                        &rt->ev_rev, &rt->ev_batch[0], &rt->ev_batch[1]})
-    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
-  rt->face_cnt.assign(face_cnt, face_cnt + nranks);
-  rt->ghost_cnt.assign(ghost_cnt, ghost_cnt + nranks);
-  rt->face_off.assign(nranks, 0);
-  rt->ghost_off.assign(nranks, 0);
-  for (int p = 1; p < nranks; ++p) {
-    rt->face_off[p] = rt->face_off[p - 1] + rt->face_cnt[p - 1];
-    rt->ghost_off[p] = rt->ghost_off[p - 1] + rt->ghost_cnt[p - 1];
-  }
-  rt->halo = nranks > 1 && (rt->face_total + rt->ghost_total) > 0;
   // overlapped schedule: x whole, so only the last tile row (y ghost plane)
   // and the last tile column (z ghost plane) touch ghosts
   const BdxLattice L = BdxLattice::from(c.latd);
@@ -1069,41 +1259,67 @@ Handle* create(const int64_t* latd, const int64_t* own, const int* iparams, doub
     std::memcpy(rt->rect_r2, r2, sizeof(r2));
     rt->split = true;
   }
-  if (transport == 1 && nranks > 1) {  // RCCL: connected by bdx_rt_connect
-    auto t = std::make_unique<RcclTransport>();
-    t->nranks = nranks;
-    rt->tr = std::move(t);
-  } else if (transport == 2 && nranks > 1) {  // in-process threads
-    auto t = std::make_unique<ThreadTransport>();
-    {
-      std::lock_guard<std::mutex> lk(g_groups_m);
-      auto& g = g_groups[group_id];
-      if (!g) {
-        g = std::make_shared<ThreadGroupState>();
-        g->size = nranks;
-        g->sbuf.assign(nranks, nullptr);
-        g->soff.assign(nranks, nullptr);
-        g->packed.assign(nranks, nullptr);
-        g->copied.assign(nranks, nullptr);
-        g->red.assign(nranks, nullptr);
-      }
-      t->g = g;
-    }
-    t->rank = rank;
-    rt->tr = std::move(t);
-  } else {  // single rank: no communication
-    rt->tr = std::make_unique<NoTransport>();
-    rt->halo = false;
-    rt->split = false;
-  }
-  return new Handle{sizeof(T) == 8, rt.release()};
+  return rt.release();
+}
+
+// iparams of the dofmap kind: P, nq, geom, n_inner, n_outer, use_graph,
+// overlap; ptrs: x, r, p_a, p_b, y, scal, partials, upart, hbuf_a, hbuf_b,
+// face_boxes, ghost_boxes, tab, inner, outer, cdofs, cverts, coords, flags, G,
+// kc (G / kc may be null)
+template <typename T>
+LoopBase* create_dofmap(const int64_t* latd, const int* iparams, int64_t nvec, double kappa,
+                        void* const* ptrs, const int64_t* halo_sizes, const int64_t* face_cnt,
+                        const int64_t* ghost_cnt, int transport, int nranks, int rank,
+                        int64_t group_id, hipStream_t st) {
+  auto rt = std::make_unique<DofCGRuntime<T>>();
+  rt->esize = sizeof(T);
+  DofConfig& c = rt->cfg;
+  std::memcpy(c.latd, latd, sizeof(c.latd));
+  c.P = iparams[0];
+  c.nq = iparams[1];
+  c.geom = iparams[2];
+  c.n_inner = iparams[3];
+  c.n_outer = iparams[4];
+  rt->use_graph = iparams[5] != 0;
+  const bool overlap = iparams[6] != 0;
+  c.nvec = nvec;
+  c.kappa = kappa;
+  c.nb_inner = bdx_dofmap_nblocks(c.nq, c.n_inner);
+  c.nb_outer = bdx_dofmap_nblocks(c.nq, c.n_outer);
+  if (c.nb_inner < 0 || c.nb_outer < 0 || c.nb_inner + c.nb_outer > bdx_hip_partials_size())
+    return nullptr;
+  int i = 0;
+  rt->x = static_cast<T*>(ptrs[i++]);
+  rt->r = static_cast<T*>(ptrs[i++]);
+  rt->pa = static_cast<T*>(ptrs[i++]);
+  rt->pb = static_cast<T*>(ptrs[i++]);
+  rt->y = static_cast<T*>(ptrs[i++]);
+  rt->scal = static_cast<double*>(ptrs[i++]);
+  rt->partials = static_cast<double*>(ptrs[i++]);
+  rt->upart = static_cast<double*>(ptrs[i++]);
+  void* const* hptrs = ptrs + i;
+  i += 4;
+  rt->tab = static_cast<const T*>(ptrs[i++]);
+  rt->inner = static_cast<const int*>(ptrs[i++]);
+  rt->outer = static_cast<const int*>(ptrs[i++]);
+  rt->cdofs = static_cast<const int*>(ptrs[i++]);
+  rt->cverts = static_cast<const int*>(ptrs[i++]);
+  rt->coords = static_cast<const T*>(ptrs[i++]);
+  rt->flags = static_cast<const unsigned char*>(ptrs[i++]);
+  rt->G = static_cast<const T*>(ptrs[i++]);
+  rt->kc = static_cast<const T*>(ptrs[i++]);
+  if (!rt->tab || !rt->cdofs || !rt->flags || (c.geom == kGeomStored && !rt->G)) return nullptr;
+  rt->wlatd = c.latd;
+  if (rt->init_common(st, hptrs, halo_sizes, face_cnt, ghost_cnt, transport, nranks, rank,
+                      group_id))
+    return nullptr;
+  rt->split = overlap && rt->halo && c.n_outer > 0;
+  return rt.release();
 }
 
 template <typename F>
 auto with_rt(void* h, F&& f) {
-  auto* H = static_cast<Handle*>(h);
-  if (H->is_f64) return f(static_cast<CGRuntime<double>*>(H->rt));
-  return f(static_cast<CGRuntime<float>*>(H->rt));
+  return f(static_cast<LoopBase*>(h));
 }
 
 }  // namespace
@@ -1175,10 +1391,22 @@ void* bdx_rt_create(int is_f64, const int64_t* latd, const int64_t* own, const i
                        ghost_cnt, transport, nranks, rank, group_id, st, latd_tiled, tptrs);
 }
 
+// The dofmap data model's CG loop (see create_dofmap for the arguments).
+void* bdx_rt_create_dofmap(int is_f64, const int64_t* latd, const int* iparams, int64_t nvec,
+                           double kappa, void* const* ptrs, const int64_t* halo_sizes,
+                           const int64_t* face_cnt, const int64_t* ghost_cnt, int transport,
+                           int nranks, int rank, int64_t group_id, hipStream_t st) {
+  if (is_f64)
+    return create_dofmap<double>(latd, iparams, nvec, kappa, ptrs, halo_sizes, face_cnt,
+                                 ghost_cnt, transport, nranks, rank, group_id, st);
+  return create_dofmap<float>(latd, iparams, nvec, kappa, ptrs, halo_sizes, face_cnt, ghost_cnt,
+                              transport, nranks, rank, group_id, st);
+}
+
 // Comm stream priority: out[0] least, out[1] greatest (device range),
 // out[2] the priority the comm stream runs at.
 int bdx_rt_comm_priority(void* h, int* out) {
-  return with_rt(h, [&](auto* rt) {
+  return with_rt(h, [&](LoopBase* rt) {
     out[0] = rt->prio_least;
     out[1] = rt->prio_greatest;
     out[2] = rt->prio_cs;
@@ -1186,27 +1414,31 @@ int bdx_rt_comm_priority(void* h, int* out) {
   });
 }
 
-// Transport pre-flight (see CGRuntime::preflight); out[2].
+// Transport pre-flight (see LoopBase::preflight); out[2].
 int bdx_rt_preflight(void* h, double timeout_s, double* out) {
-  return with_rt(h, [&](auto* rt) { return rt->preflight(timeout_s, out); });
+  return with_rt(h, [&](LoopBase* rt) { return rt->preflight(timeout_s, out); });
 }
 
-// Comm/compute overlap probe on one GPU (see CGRuntime::overlap_probe);
-// buf: 2 n doubles; out[5].
+// Comm/compute overlap probe on one GPU (see CGRuntime::overlap_probe;
+// fused operators only); buf: 2 n doubles; out[5].
 int bdx_rt_overlap_probe(void* h, int64_t n, double* buf, int reps, double* out) {
-  return with_rt(h, [&](auto* rt) { return rt->overlap_probe(n, buf, reps, out); });
+  return with_rt(h, [&](LoopBase* rt) -> int {
+    if (auto* f = dynamic_cast<CGRuntime<double>*>(rt)) return f->overlap_probe(n, buf, reps, out);
+    if (auto* f = dynamic_cast<CGRuntime<float>*>(rt)) return f->overlap_probe(n, buf, reps, out);
+    return static_cast<int>(hipErrorInvalidValue);
+  });
 }
 
 // 1 if the loop runs on the tiled storage layout.
 int bdx_rt_tiled(void* h) {
-  return with_rt(h, [](auto* rt) { return rt->tiled ? 1 : 0; });
+  return with_rt(h, [](LoopBase* rt) { return rt->tiled() ? 1 : 0; });
 }
 
 // Open the runtime's RCCL communicator (collective over the ranks; every
 // rank calls it only after all ranks created their runtime).  Bounded by the
 // watchdog deadline.  0 on success (or when the transport is not RCCL).
 int bdx_rt_connect(void* h, const void* uid, int rank) {
-  return with_rt(h, [&](auto* rt) -> int {
+  return with_rt(h, [&](LoopBase* rt) -> int {
     auto* t = dynamic_cast<RcclTransport*>(rt->tr.get());
     if (!t) return 0;
     ncclUniqueId id;
@@ -1217,20 +1449,21 @@ int bdx_rt_connect(void* h, const void* uid, int rank) {
 
 // Ranks of the transport (ncclCommCount for RCCL; -1 if not connected).
 int bdx_rt_comm_count(void* h) {
-  return with_rt(h, [](auto* rt) { return rt->tr->ranks(); });
+  return with_rt(h, [](LoopBase* rt) { return rt->tr->ranks(); });
 }
 
-// 1 if the overlapped (split-tile, two-stream) schedule is active.
+// 1 if the overlapped (split, two-stream) schedule is active.
 int bdx_rt_overlap(void* h) {
-  return with_rt(h, [](auto* rt) { return rt->split ? 1 : 0; });
+  return with_rt(h, [](LoopBase* rt) { return rt->split ? 1 : 0; });
 }
 
 // Reset the CG state after a new prologue (p_a zeroed by the caller).
 int bdx_rt_reset(void* h) {
-  return with_rt(h, [](auto* rt) {
+  return with_rt(h, [](LoopBase* rt) {
     rt->it = 0;
     rt->pend = 0;
-    rt->need_import = rt->tiled;  // the new prologue's r and x, at the next iterate
+    if (auto* f = dynamic_cast<CGRuntime<double>*>(rt)) f->need_import = f->is_tiled;
+    if (auto* f = dynamic_cast<CGRuntime<float>*>(rt)) f->need_import = f->is_tiled;
     return 0;
   });
 }
@@ -1238,54 +1471,62 @@ int bdx_rt_reset(void* h) {
 // Bind a new iterate buffer x (DeviceCG.start with another x): the captured
 // graphs hold the old pointer, so they are dropped and re-captured.
 int bdx_rt_bind_x(void* h, void* x) {
-  return with_rt(h, [&](auto* rt) {
-    using T = std::remove_pointer_t<decltype(rt->x)>;
-    if (rt->x != static_cast<T*>(x)) {
-      const hipError_t e = hipStreamSynchronize(rt->st);
-      rt->drop_graphs();
-      rt->x = static_cast<T*>(x);
-      if (!rt->tiled) rt->wx = rt->x;
+  return with_rt(h, [&](LoopBase* rt) -> int {
+    auto rebind = [&](auto* f) -> int {
+      using T = std::remove_pointer_t<decltype(f->x)>;
+      if (f->x == static_cast<T*>(x)) return 0;
+      const hipError_t e = hipStreamSynchronize(f->st);
+      f->drop_graphs();
+      f->x = static_cast<T*>(x);
+      if constexpr (std::is_same_v<std::remove_pointer_t<decltype(f)>, CGRuntime<T>>) {
+        if (!f->is_tiled) f->wx = f->x;
+      }
       return static_cast<int>(e);
-    }
-    return 0;
+    };
+    if (auto* f = dynamic_cast<CGRuntime<double>*>(rt)) return rebind(f);
+    if (auto* f = dynamic_cast<CGRuntime<float>*>(rt)) return rebind(f);
+    if (auto* f = dynamic_cast<DofCGRuntime<double>*>(rt)) return rebind(f);
+    if (auto* f = dynamic_cast<DofCGRuntime<float>*>(rt)) return rebind(f);
+    return static_cast<int>(hipErrorInvalidValue);
   });
 }
 
 int bdx_rt_iterate(void* h, long n) {
-  return with_rt(h, [&](auto* rt) { return rt->iterate(n); });
+  return with_rt(h, [&](LoopBase* rt) { return rt->iterate(n); });
 }
 
 // iterate() plus the device time of each of the n steps (timing events
 // between the steps, read after a bounded host wait): step_ms[n]
 int bdx_rt_iterate_timed(void* h, long n, float* step_ms) {
-  return with_rt(h, [&](auto* rt) { return rt->iterate(n, step_ms); });
+  return with_rt(h, [&](LoopBase* rt) { return rt->iterate(n, step_ms); });
 }
 
 // Host wait for everything iterate() queued, bounded by the RCCL deadline
 // (a hung peer aborts the communicator instead of blocking forever).
 int bdx_rt_wait(void* h) {
-  return with_rt(h, [](auto* rt) { return rt->tr->wait(rt->ev_out); });
+  return with_rt(h, [](LoopBase* rt) { return rt->tr->wait(rt->ev_out); });
 }
 
 // n eager CG iterations with hipEvent phase timers; out (13 doubles, mean ms):
 //   0 forward halo (comm stream: pack, exchange, unpack)
-//   1 operator, interior tiles A (serial schedule: the whole operator)
-//   2 ghost-touching tiles + ghost finalize (waits for the forward halo)
+//   1 operator, interior tiles / cells (serial schedule: the first launch)
+//   2 boundary work: split: ghost-touching tiles / cells (+ ghost fold)
+//     after the forward halo; serial: what follows the first launch
 //   3 reverse halo (pack, exchange; serial: + unpack-add)
-//   4 operator, interior tiles B
-//   5 unpack-add + reduce + all-reduce(p.Ap) (waits for the reverse halo)
+//   4 interior done -> comm stream joined, received sums added
+//   5 reduce + all-reduce(p.Ap)
 //   6 r update + r.r
 //   7 all-reduce(r.r)
 //   8 whole iteration
-//   9..12 end of the forward halo / interior tiles A / reverse halo / interior
-//         tiles B, measured from the iteration start (overlap evidence)
+//   9..12 end of the forward halo / boundary work / reverse halo / interior
+//         work, measured from the iteration start (overlap evidence)
 int bdx_rt_profile(void* h, long n, double* out, int nout) {
-  return with_rt(h, [&](auto* rt) { return rt->profile(n, out, nout); });
+  return with_rt(h, [&](LoopBase* rt) { return rt->profile(n, out, nout); });
 }
 
 // it (iterations done) and whether steady-state graphs are in use.
 int bdx_rt_state(void* h, long* it, int* graphs) {
-  return with_rt(h, [&](auto* rt) {
+  return with_rt(h, [&](LoopBase* rt) {
     *it = rt->it;
     *graphs = rt->use_graph &&
               (rt->graph_ok[0] || rt->graph_ok[1] || rt->graph_ok[2] || rt->graph_ok[3]);
@@ -1293,15 +1534,7 @@ int bdx_rt_state(void* h, long* it, int* graphs) {
   });
 }
 
-void bdx_rt_destroy(void* h) {
-  auto* H = static_cast<Handle*>(h);
-  if (!H) return;
-  if (H->is_f64)
-    delete static_cast<CGRuntime<double>*>(H->rt);
-  else
-    delete static_cast<CGRuntime<float>*>(H->rt);
-  delete H;
-}
+void bdx_rt_destroy(void* h) { delete static_cast<LoopBase*>(h); }
 
 void bdx_rt_release_group(int64_t group_id) {
   std::lock_guard<std::mutex> lk(g_groups_m);

@@ -120,13 +120,19 @@ class DofmapLaplacianGPU:
     csrc/hip/lap_dofmap.h): p = r + beta p_old, the lagged x update and the
     p.Ap element dots ride in the gather / scatter of the operator kernel, and
     one update pass does r -= alpha y, r.r and y = 0 -- the reference's five
-    BLAS-1 calls per iteration (src/cg.hpp:121-167) become one.
+    BLAS-1 calls per iteration (src/cg.hpp:121-167) become one.  The
+    iteration loop runs in the native C++ runtime (runtime.hip DofCGRuntime:
+    interior cells on the compute stream, forward exchange -> boundary cells
+    -> reverse send on the comm stream, device all-reduces, watchdog);
+    `runtime="python"` (or BDX_DOFMAP_RUNTIME=python) drives the same kernels
+    from Python with torch collectives.
     """
 
     name = "dofmap"
     RR0, RR1, PAP = 0, 1, 2  # DeviceCG's scalar slots
 
-    def __init__(self, problem, geometry: str = "otf", mesh: UnstructuredMesh | None = None):
+    def __init__(self, problem, geometry: str = "otf", mesh: UnstructuredMesh | None = None,
+                 runtime: str | None = None):
         if problem.platform != "gpu":
             raise ValueError("DofmapLaplacianGPU needs the GPU platform")
         if geometry not in ("otf", "stored"):
@@ -158,6 +164,15 @@ class DofmapLaplacianGPU:
                 self.k.dofmap_geometry(m.ncells, self.cverts, self.coords, self.G)
                 self.geom = 0
         self._cg = None
+        self._rt = None
+        import os
+        self.runtime = runtime or os.environ.get("BDX_DOFMAP_RUNTIME", "native")
+
+    def close(self) -> None:
+        """Release the native runtime (RCCL communicator, streams)."""
+        if self._rt is not None:
+            self._rt.close()
+            self._rt = None
 
     def _run(self, cells, u, y, **kw) -> int:
         n = int(cells.numel())
@@ -184,16 +199,38 @@ class DofmapLaplacianGPU:
         k.dot(cg.r, cg.r, cg.partials, cg.scal, self.RR0)
         cg._allreduce(self.RR0)
         n = pb.lat.nstore
-        self.p_a = torch.zeros(n, dtype=pb.dtype, device=pb.device)
-        self.p_b = torch.zeros(n, dtype=pb.dtype, device=pb.device)
-        self.part = torch.zeros(int(cg.partials.numel()), dtype=torch.float64, device=pb.device)
+        if getattr(self, "p_a", None) is None:
+            # allocated once: the native runtime keeps pointers to them
+            self.p_a = torch.zeros(n, dtype=pb.dtype, device=pb.device)
+            self.p_b = torch.zeros(n, dtype=pb.dtype, device=pb.device)
+            self.part = torch.zeros(int(cg.partials.numel()), dtype=torch.float64,
+                                    device=pb.device)
+        else:
+            self.p_a.zero_()  # p_old of the first iteration (beta = 0 still reads it)
         cg.y.zero_()
         self.x_lag = False
         self._cg = cg
+        if self.runtime == "native":
+            if self._rt is None or self._rt.cg is not cg:
+                from ..solvers.native import NativeCGRuntime, NativeRuntimeUnavailable
+                if self._rt is not None:
+                    self._rt.close()
+                try:
+                    self._rt = NativeCGRuntime(self, cg)
+                except NativeRuntimeUnavailable as e:
+                    import sys
+                    print(f"[bdx] native CG runtime unavailable ({e}); using the Python "
+                          f"driver of the dofmap kernels", file=sys.stderr)
+                    self.runtime, self._rt = "python", None
+            if self._rt is not None:
+                self._rt.bind_x(x)
+                self._rt.reset()
 
     def cg_iterate(self, cg, n: int, flush: bool = True) -> None:
         """n fused CG iterations; `flush=False` leaves the last lagged x
         update pending (a later call or `flush` applies it)."""
+        if self._rt is not None:
+            return self._rt.iterate(n)
         pb, k = self.pb, self.k
         r, y, x, scal = cg.r.view(-1), cg.y.view(-1), cg.x.view(-1), cg.scal
         for _ in range(n):

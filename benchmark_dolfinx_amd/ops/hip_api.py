@@ -77,6 +77,9 @@ def declare(lib) -> None:
     _d(lib, "bdx_rt_rccl_selftest", [vp, i32, vp])
     _d(lib, "bdx_rt_create", [i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
                               i64, vp, vp, vp], vp)
+    _d(lib, "bdx_rt_create_dofmap", [i32, vp, vp, i64, f64, vp, vp, vp, vp, i32, i32, i32, i64,
+                                     vp], vp)
+    _d(lib, "bdx_dofmap_nblocks", [i32, i32])
     _d(lib, "bdx_rt_tiled", [vp])
     _d(lib, "bdx_rt_connect", [vp, vp, i32])
     _d(lib, "bdx_rt_comm_count", [vp])

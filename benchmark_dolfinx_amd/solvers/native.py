@@ -77,18 +77,61 @@ class NativeCGRuntime:
             use_graph = mode == "2" or (mode == "1" and comm.size == 1)
         if overlap is None:
             overlap = os.environ.get("BDX_OVERLAP", "1") != "0"
-        t = op.t
+        self.kind = "dofmap" if getattr(op, "name", "") == "dofmap" else "fused"
+        self.group = 0
+        if comm.size == 1:
+            transport = 0
+        elif hasattr(comm, "g"):  # ThreadComm: ranks are threads of this process
+            transport = 2
+            self.group = comm.g.uid  # unique per group: a reused id() could
+            # pick up a stale group of a runtime that was not closed yet
+        elif comm.backend == "nccl":
+            transport = 1
+        else:
+            transport = -1
+        self.transport = {0: "none", 1: "rccl", 2: "thread"}.get(transport, "unsupported")
+        self.upart = torch.zeros(self.lib.bdx_hip_partials_size(), dtype=torch.float64,
+                                 device=pb.device)
+        self.x = cg.x
+        fo, gh = halo.owned_faces, halo.ghosts
+        self._hs = np.array([len(fo.boxes), fo.total, len(gh.boxes), gh.total], dtype=np.int64)
+        self._fc = np.array(fo.counts, dtype=np.int64)
+        self._gc = np.array(gh.counts, dtype=np.int64)
         self._latd = np.ascontiguousarray(pb.latd, dtype=np.int64)
+        ok = transport >= 0 and comm.rank != self._inject_fail_rank
+        if self.kind == "dofmap":
+            ok = ok and self._create_dofmap(op, cg, use_graph, overlap, transport)
+        else:
+            ok = ok and self._create_fused(op, cg, use_graph, overlap, transport)
+        self._connect(comm, ok, transport)
+
+    def _create_dofmap(self, op, cg, use_graph, overlap, transport) -> bool:
+        """The dofmap data model's loop (runtime.hip DofCGRuntime)."""
+        pb, halo = self.pb, self.pb.halo
+        self.tiled = False
+        self._ip = np.array([pb.degree, pb.tables.nq, op.geom, int(op.inner.numel()),
+                             int(op.outer.numel()), int(use_graph), int(overlap)], dtype=np.int32)
+        bufs = [cg.x, cg.r, op.p_a, op.p_b, cg.y, cg.scal, cg.partials, self.upart,
+                halo.buf_a, halo.buf_b, halo.owned_faces.table, halo.ghosts.table, op.tab,
+                op.inner, op.outer, op.cdofs, op.cverts, op.coords, op.flags, op.G, op.kc]
+        self._keep = bufs
+        self._ptrs = (ctypes.c_void_p * len(bufs))(*[ptr(b) for b in bufs])
+        self.h = self.lib.bdx_rt_create_dofmap(
+            int(pb.dtype == torch.float64), ptr(self._latd), ptr(self._ip), int(cg.r.numel()),
+            float(pb.kappa), self._ptrs, ptr(self._hs), ptr(self._fc), ptr(self._gc), transport,
+            pb.comm.size, pb.comm.rank, self.group, _stream())
+        return bool(self.h)
+
+    def _create_fused(self, op, cg, use_graph, overlap, transport) -> bool:
+        pb, halo = self.pb, self.pb.halo
+        t = op.t
         self._own = np.array(pb.lat.owned_hi, dtype=np.int64)
         self._ip = np.array([op.version, op.affine_code, pb.degree, t.nq, op.nblocks, op.nty,
                              op.ntz, op.sy, op.sz, int(use_graph), int(overlap), op.nseg],
                             dtype=np.int32)
         self._wts = np.ascontiguousarray(t.wts, dtype=np.float64)
         self._qpts = np.ascontiguousarray(t.qpts, dtype=np.float64)
-        self.upart = torch.zeros(self.lib.bdx_hip_partials_size(), dtype=torch.float64,
-                                 device=pb.device)
         fo, gh = halo.owned_faces, halo.ghosts
-        self.x = cg.x
         # Tiled vector storage for the x-march kernels: each (y, z) tile's
         # patch of an x-plane is contiguous, so the kernels' writes are whole
         # lines (profiles/r2_march_bw.md).  BDX_TILED=0: the lattice layout;
@@ -114,30 +157,18 @@ class NativeCGRuntime:
                 op.partials, self.upart, halo.buf_a, halo.buf_b, fo.table, gh.table, pb.kc]
         self._keep = bufs + [op.tabs]
         self._ptrs = (ctypes.c_void_p * len(bufs))(*[ptr(b) for b in bufs])
-        self._hs = np.array([len(fo.boxes), fo.total, len(gh.boxes), gh.total], dtype=np.int64)
-        self._fc = np.array(fo.counts, dtype=np.int64)
-        self._gc = np.array(gh.counts, dtype=np.int64)
-        self.group = 0
-        if comm.size == 1:
-            transport = 0
-        elif hasattr(comm, "g"):  # ThreadComm: ranks are threads of this process
-            transport = 2
-            self.group = comm.g.uid  # unique per group: a reused id() could
-            # pick up a stale group of a runtime that was not closed yet
-        elif comm.backend == "nccl":
-            transport = 1
-        else:
-            transport = -1
-        self.transport = {0: "none", 1: "rccl", 2: "thread"}.get(transport, "unsupported")
-        # 1) local creation (no communication)
-        ok = transport >= 0 and comm.rank != self._inject_fail_rank
-        if ok:
-            self.h = self.lib.bdx_rt_create(
-                int(pb.dtype == torch.float64), ptr(self._latd), ptr(self._own), ptr(self._ip),
-                float(pb.kappa), ptr(self._wts), ptr(self._qpts), ptr(op.tabs), self._ptrs,
-                ptr(self._hs), ptr(self._fc), ptr(self._gc), transport, comm.size, comm.rank,
-                self.group, _stream(), ptr(self._latdT), self._tptrs)
-            ok = bool(self.h)
+        del fo, gh
+        self.h = self.lib.bdx_rt_create(
+            int(pb.dtype == torch.float64), ptr(self._latd), ptr(self._own), ptr(self._ip),
+            float(pb.kappa), ptr(self._wts), ptr(self._qpts), ptr(op.tabs), self._ptrs,
+            ptr(self._hs), ptr(self._fc), ptr(self._gc), transport, pb.comm.size, pb.comm.rank,
+            self.group, _stream(), ptr(self._latdT), self._tptrs)
+        return bool(self.h)
+
+    def _connect(self, comm, ok: bool, transport: int) -> None:
+        """1) every rank created its runtime locally (no communication): agree;
+        2) open the RCCL communicator (ncclUniqueId from rank 0 over the torch
+        group), bounded by the watchdog deadline: agree again."""
         if not _agree(comm, ok):
             self.close()
             raise NativeRuntimeUnavailable(

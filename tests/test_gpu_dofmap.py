@@ -75,26 +75,38 @@ def test_dofmap_equivariant_under_renumbering(P, pert):
     assert (got - ref).abs().max().item() <= 1e-12 * ref.abs().max().item()
 
 
-def _cg_job(comm, nc, P, nits, pert):
+def _cg_job(comm, nc, P, nits, pert, runtime="native"):
     pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", pert, "random")
     u = pb.assemble_rhs()
     x = pb.new_vector()
-    op = DofmapLaplacianGPU(pb)
+    op = DofmapLaplacianGPU(pb, runtime=runtime)
     cg = DeviceCG(pb)
     cg.solve(op, x, u, nits)
     cg.wait()
-    return pb.norm(x), len(op.mesh.boundary_cells)
+    rt = op._rt
+    info = (rt.transport, rt.overlap) if rt is not None else None
+    op.close()
+    return pb.norm(x), len(op.mesh.boundary_cells), info
 
 
+@pytest.mark.parametrize("runtime", ["native", "python"])
 @pytest.mark.parametrize("ranks", [2, 4])
-def test_dofmap_partition_invariance_threaded(ranks):
+def test_dofmap_partition_invariance_threaded(ranks, runtime):
+    """Thread ranks on one GPU; `native`: the C++ loop (DofCGRuntime) with its
+    split schedule (interior cells || forward exchange -> boundary cells ->
+    reverse send), `python`: the same kernels driven with torch collectives."""
     ref = run_threaded(1, _cg_job, (5, 6, 7), 3, 12, 0.15)[0][0]
-    got = run_threaded(ranks, _cg_job, (5, 6, 7), 3, 12, 0.15)
-    assert any(nb > 0 for _, nb in got)  # the overlapped boundary pass ran
-    for xn, _ in got:
+    got = run_threaded(ranks, _cg_job, (5, 6, 7), 3, 12, 0.15, runtime)
+    assert any(nb > 0 for _, nb, _ in got)  # the overlapped boundary pass ran
+    for xn, _, info in got:
         assert abs(xn - ref) <= 1e-11 * abs(ref), (xn, ref)
+        if runtime == "native":
+            assert info is not None and info[0] == "thread", info
+    if runtime == "native":
+        assert any(info[1] for _, _, info in got)  # the two-stream schedule ran
 
 
+@pytest.mark.parametrize("runtime", ["native", "python"])
 @pytest.mark.parametrize("nc,P,qm,geometry,dt,kappa", [
     ((4, 3, 5), 3, 1, "stored", torch.float64, "constant"),
     ((4, 3, 5), 3, 1, "otf", torch.float64, "random"),
@@ -103,16 +115,18 @@ def test_dofmap_partition_invariance_threaded(ranks):
     ((2, 2, 2), 7, 1, "otf", torch.float64, "constant"),
     ((3, 4, 3), 3, 1, "stored", torch.float32, "constant"),
 ])
-def test_dofmap_cg_matches_host_cg(nc, P, qm, geometry, dt, kappa):
+def test_dofmap_cg_matches_host_cg(nc, P, qm, geometry, dt, kappa, runtime):
     """The fused dofmap CG iteration (p update, lagged x, p.Ap element dots
-    and the r / y update pass) against the host CG on the CPU operator."""
+    and the r / y update pass), in the native C++ loop and driven from
+    Python, against the host CG on the CPU operator."""
     gpu = PoissonProblem(Comm(), nc, P, qm, False, dt, "gpu", 0.1, kappa)
     cpu = PoissonProblem(Comm(), nc, P, qm, False, torch.float64, "cpu", 0.1, kappa)
     ug, uc = gpu.assemble_rhs(), cpu.assemble_rhs()
     xg, xc = gpu.new_vector(), cpu.new_vector()
-    op = DofmapLaplacianGPU(gpu, geometry)
+    op = DofmapLaplacianGPU(gpu, geometry, runtime=runtime)
     cg = DeviceCG(gpu)
     cg.start(op, xg, ug)
+    assert (op._rt is not None) == (runtime == "native")
     cg.iterate(7)   # two calls: the lagged x update is flushed and resumed
     ms = cg.iterate_timed(13)  # per-step calls, one flush at the end (bench path)
     assert len(ms) == 13
