@@ -9,11 +9,14 @@ tag=$1; args=$2; lib=${3:-}
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
 P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE"
 P3="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE"
-P4="FETCH_SIZE WRITE_SIZE"
+# FETCH_SIZE takes 3 of the 4 TCC slots and WRITE_SIZE 2: one pass each
+P4="FETCH_SIZE"
+P5="WRITE_SIZE"
 if [ -n "$lib" ]; then
   export BDX_HIP_LIB=benchmark_dolfinx_amd/ops/libbdx_hip_$lib.so BDX_ALLOW_VARIANT=1
 fi
-for pass in 1 2 3 4; do
+passes=${PMC_PASSES:-1 2 3 4 5}
+for pass in $passes; do
   eval "ctrs=\$P$pass"
   step pmc_${tag}_$pass 180 timeout -s KILL 170 rocprofv3 --pmc $ctrs --output-format csv \
     -d gpurun_out/pmc_${tag}/p$pass -o pmc -- python3 bench.py $args --companions off --extras off --profile-steps 0
