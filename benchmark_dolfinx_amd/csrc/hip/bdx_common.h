@@ -21,6 +21,18 @@ constexpr int kFusedTabMax = 2 * 9 * 12 + 9 * 8 + 8 * 12;
 
 enum { kGeomStored = 0, kGeomOTF = 1 };
 
+// FP64 MFMA operand / accumulator vectors (v_mfma_f64_16x16x4f64: 4 results per lane)
+typedef double bdx_f64x4 __attribute__((ext_vector_type(4)));
+typedef double bdx_f64x2 __attribute__((ext_vector_type(2)));
+
+// Value of lane (l ^ 8) within each 16-lane row (DPP row_ror:8 = swap of the
+// row halves; two VALU moves per double, no LDS).
+__device__ __forceinline__ double dpp_row_ror8(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x128, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x128, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
 // Lagged x update of the fused5 CG (Fused2Args::xmode, bits 4-5 of the apply
 // entry points' mode word, set by runtime.hip): one term per iteration, save
 // alpha_prev only, or fold two terms; the saved alpha's slot of the CG scalars.

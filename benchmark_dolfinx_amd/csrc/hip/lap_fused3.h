@@ -47,6 +47,18 @@ template <int NQ, int AFF> struct Fused3Waves {
 // The gather and staging descriptors are re-materialised every layer through
 // an empty asm (the descriptor laundering of lap_fused5.h).
 
+// y / z contraction stages of the FP64 Q6 (NQ = 8, one cell per wave)
+// instances on the matrix pipe (v_mfma_f64_16x16x4f64, [B; Dd] stacked into
+// the 16-row operand) instead of the VALU.  Same-box A/B, Q6 500 M perturbed
+// (x-trilinear), 3 interleaved runs each, GDoF/s (profiles/r4_fused3_mfma.md):
+// VALU 30.2; front z 30.4; back z 30.1; front + back z 30.6; front z + back y
+// + back z 30.9 (adopted); all four 30.2 (the front-y stage's lane exchange
+// stalls on its MFMA results).
+constexpr bool kF3MfmaFrontZ = true;
+constexpr bool kF3MfmaFrontY = false;
+constexpr bool kF3MfmaBackY = true;
+constexpr bool kF3MfmaBackZ = true;
+
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
 __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fused3Waves<NQ, AFF>::value))
@@ -66,6 +78,15 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
   // intra-cell stages only exchange data inside a wave when a cell's NQ^2
   // columns tile whole waves
   constexpr bool WAVELOCAL = (64 % NQ2 == 0) && (S::lanes % 64 == 0);
+  // front z on the matrix pipe: FP64 cells that are one wave each (Q6 qmode=1)
+  // y / z contraction stages on the matrix pipe (see kF3Mfma*): FP64 cells
+  // that are one wave each (Q6 qmode=1), x-trilinear and parallelepiped
+  // instances (the general trilinear instance measured 1.3 % slower with them)
+  constexpr bool MFOK = sizeof(T) == 8 && NQ == 8 && ND == 7 && WAVELOCAL && AFF != 0;
+  constexpr bool MFZ = kF3MfmaFrontZ && MFOK;
+  constexpr bool MFY = kF3MfmaFrontY && MFOK;
+  constexpr bool MFBY = kF3MfmaBackY && MFOK;
+  constexpr bool MFBZ = kF3MfmaBackZ && MFOK;
   // LDS work buffers of the contraction core: NBUFS buffers W[k][cell][i1][i2]
   // of rows of ND values.  Padded for conflict-free 16-byte LDS access
   // (scripts/lds_bank_sim.py; measured: unpadded Q6 lost 56 % of its LDS
@@ -387,8 +408,49 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
     };
 
     // ------------------------------------------------ front z: (B_z u, Dd_z u)
-    // lanes (c, j = a < ND, qz = b): rows over the cell's x dofs i
-    if (lane_on && a < ND) {
+    if constexpr (MFZ) {
+      // matrix pipe (one cell per wave, FP64, NQ = 8):
+      //   C[(B | Dd, qz)][(i, j)] = [B; Dd] (16 x 8, k = 7 zero) . u[k][(i, j)]
+      // 4 column tiles of 16 (i, j) pairs x 2 k-steps of v_mfma_f64_16x16x4f64;
+      // the stacked table is the constant A operand (lane: row n, k = g), the
+      // u column the B operand (lane: k = g, column n), one scalar LDS read
+      // per MFMA instead of the VALU form's ND^2 reads and 2 ND^2 FMAs per lane.
+      // Result rows g + 4r: r = 0, 1 -> B_z u at qz = g, g + 4; r = 2, 3 -> Dd_z u.
+      int ltid = tid;
+      asm volatile("" : "+v"(ltid));  // lane roles and operands re-derived per layer, not hoisted
+      const int mg = (ltid & 63) >> 4, mn = ltid & 15;
+      const T* __restrict__ arow = s_tab + (mn < NQ ? OFF_BR + mn * NP : OFF_DR + (mn - NQ) * NP);
+      const double a0 = arow[mg];
+      const double a1 = mg + 4 < ND ? arow[mg + 4] : 0.0;
+      const int kb = mg + 4 < ND ? mg + 4 : ND - 1;  // k = 7: finite operand, zero row of A
+      const T* __restrict__ ub = su + ycell * DZP + zcell;
+      constexpr int NTL = (ND * ND + 15) / 16;
+      bdx_f64x4 acc[NTL];
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {  // first k-step of every tile, then the second
+        const int cc = t * 16 + mn < ND * ND ? t * 16 + mn : ND * ND - 1;
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, ub[(cc / ND) * PLP + (cc % ND) * DZP + mg],
+                                                      bdx_f64x4{0, 0, 0, 0}, 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {
+        const int cc = t * 16 + mn < ND * ND ? t * 16 + mn : ND * ND - 1;
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, ub[(cc / ND) * PLP + (cc % ND) * DZP + kb],
+                                                      acc[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {
+        const int col = t * 16 + mn;
+        if (col < ND * ND) {
+          const int ii = col / ND, jj = col - (col / ND) * ND;
+          W0[offA(c, jj, mg) + ii] = acc[t][0];
+          W0[offA(c, jj, mg + 4) + ii] = acc[t][1];
+          W1[offA(c, jj, mg) + ii] = acc[t][2];
+          W1[offA(c, jj, mg + 4) + ii] = acc[t][3];
+        }
+      }
+    } else if (lane_on && a < ND) {
+      // lanes (c, j = a < ND, qz = b): rows over the cell's x dofs i
       const T* __restrict__ br = s_tab + OFF_BR + b * NP;
       const T* __restrict__ dr = s_tab + OFF_DR + b * NP;
       T ob[ND], od[ND];
@@ -418,7 +480,56 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
     // spill (61 VGPRs), so it keeps the zeroed accumulators.
     constexpr bool PEEL = AFF != 0;
     T tBB[ND], tDB[ND], tBD[ND];
-    {
+    // lane roles (qy, qz) = (xa, xb) of the geometry and x stages
+    int xa = a, xb = b;
+    if constexpr (MFY) {
+      // matrix pipe: [tBB | tDB](qz, i; qy) = E[(qz, i)][j] . [B | Dd]^T[j][qy] (E = B_z u,
+      // W0) and tBD from F = Dd_z u (W1) the same way (its Dd half unused).
+      // Row tiles (s, h): row m = (qz = (m & 3) + 4 s, i = (m >> 2) + 4 h), so lane
+      // (g, n) ends with the i-lines at qz = g + 4 s of column n: B rows (qy = n)
+      // in lanes n < 8, Dd rows (qy = n - 8) in lanes n >= 8.  Lane n < 8 takes
+      // (qy, qz) = (n, g), lane n >= 8 (n - 8, g + 4); the halves of each
+      // 16-lane row swap the line the partner needs (DPP row rotate by 8).
+      int ltid = tid;
+      asm volatile("" : "+v"(ltid));
+      const int mg = (ltid & 63) >> 4, mn = ltid & 15;
+      const bool lo = mn < NQ;
+      xa = mn & (NQ - 1);
+      xb = mg + (lo ? 0 : 4);
+      const T* __restrict__ brow = s_tab + (lo ? OFF_BR + mn * NP : OFF_DR + (mn - NQ) * NP);
+      const double by0 = brow[mg];
+      const double by1 = mg + 4 < ND ? brow[mg + 4] : 0.0;
+      const int kb = mg + 4 < ND ? mg + 4 : ND - 1;
+      auto tiles = [&](const T* __restrict__ Wsrc, int sq, T (&out)[ND]) __attribute__((always_inline)) {
+        const int qz = (mn & 3) + 4 * sq;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ii = (mn >> 2) + 4 * h < ND ? (mn >> 2) + 4 * h : ND - 1;
+          bdx_f64x4 acc = {0, 0, 0, 0};
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Wsrc[offA(c, mg, qz) + ii], by0, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Wsrc[offA(c, kb, qz) + ii], by1, acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r + 4 * h < ND) out[r + 4 * h] = acc[r];
+        }
+      };
+      T e1[ND], f1[ND], f0[ND], e0[ND];
+      tiles(W1, 1, f1);  // F at qz = g + 4: the lower half's tBD, sent up
+      tiles(W1, 0, f0);
+      tiles(W0, 1, e1);
+      tiles(W0, 0, e0);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const T rcv = dpp_row_ror8(f1[i]);
+        tBD[i] = lo ? f0[i] : rcv;
+      }
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const T rcv = dpp_row_ror8(lo ? e1[i] : e0[i]);
+        tBB[i] = lo ? e0[i] : rcv;
+        tDB[i] = lo ? rcv : e1[i];
+      }
+    } else {
       const T* __restrict__ bra = s_tab + OFF_BR + a * NP;
       const T* __restrict__ dra = s_tab + OFF_DR + a * NP;
       auto row = [&](int j, bool first) __attribute__((always_inline)) {
@@ -452,7 +563,7 @@ BDX_PRAGMA_UNROLL((PEEL ? 3 : 2))
     // G = kappa w_a w_b adj(J) adj(J)^T / det J is formed once per thread and
     // layer; per point only the weight w_q remains (same operator, same maths).
     T Gc[6] = {0, 0, 0, 0, 0, 0};
-    const T kwyz = kc_cur * s_qw[NQ + a] * s_qw[NQ + b];
+    const T kwyz = kc_cur * s_qw[NQ + xa] * s_qw[NQ + xb];
     {
       const T* X0 = sX;
       const T* X1 = sX + NV;
@@ -488,7 +599,7 @@ BDX_PRAGMA_UNROLL((PEEL ? 3 : 2))
         // produces.  J = [[x_s, x_t, x_u], [0, hy, 0], [0, 0, hz]] with x_s
         // constant along the thread's x column and x_t, x_u linear in s; the
         // zero entries of the trilinear form below are dropped.
-        const T t = s_qw[a], uu = s_qw[b];
+        const T t = s_qw[xa], uu = s_qw[xb];
         const int v11 = v10 + 3;
         const T X000 = X0[v00], X001 = X0[v01], X010 = X0[v10], X011 = X0[v11];
         const T X100 = X1[v00], X101 = X1[v01], X110 = X1[v10], X111 = X1[v11];
@@ -508,7 +619,7 @@ BDX_PRAGMA_UNROLL((PEEL ? 3 : 2))
         xcu1 = xu1 * xihz;
         xcs = kwyz * xs * hy * hz;
       } else {
-        const T t = s_qw[a], uu = s_qw[b];
+        const T t = s_qw[xa], uu = s_qw[xb];
         const int v11 = v10 + 3;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -594,57 +705,115 @@ BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
       // W0 <- A1, W1 <- A2 (the front-y reads of this wave are already issued)
       wave_order();
       if (lane_on) {
-        strow<ND>(W0 + offA(c, a, b), a1);
-        strow<ND>(W1 + offA(c, a, b), a2);
+        strow<ND>(W0 + offA(c, xa, xb), a1);
+        strow<ND>(W1 + offA(c, xa, xb), a2);
       }
       cell_sync();
-      // back y, pass 1: C1 = B_y^T A1 + Dd_y^T A2 -> W0; then A3 -> W1
-      T c1[ND];
+      if constexpr (MFBY) {
+        // back y on the matrix pipe: C[(qz, i)][j] = A[(qz, i)][(src, qy)] . [B; Dd][(src, qy)][j]
+        // (column tiles of 16 (qz, i) pairs, e = 7 qz + i; the table is the
+        // constant B operand, zero for j >= ND).  Pass 1: C1 from A1 (W0) and
+        // A2 (W1), 4 k-steps, in place into W0; then A3 -> W1; pass 2: C3 from
+        // A3, 2 k-steps, in place into W1.  Lane (g, n) ends with
+        // C[(qz, i) = 16 t + g + 4 r][j = n].
+        int ltid = tid;
+        asm volatile("" : "+v"(ltid));
+        const int mg = (ltid & 63) >> 4, mn = ltid & 15;
+        constexpr int NE = NQ * ND, NTL = (NE + 15) / 16;
+        auto pass = [&](int nks, const T* __restrict__ Wk0, const T* __restrict__ Wk1, T* __restrict__ Wout)
+            __attribute__((always_inline)) {
+          double bk[4];
 #pragma unroll
-      for (int i = 0; i < ND; ++i) c1[i] = T(0);
-      if (lane_on && a < ND) {
-        const T* bcj = s_tab + OFF_BC + a * XP;
-        const T* dcj = s_tab + OFF_DC + a * XP;
-BDX_PRAGMA_UNROLL(2)
-        for (int qy = 0; qy < NQ; ++qy) {
-          T r1[ND], r2[ND];
-          ldrow<ND>(W0 + offA(c, qy, b), r1);
-          ldrow<ND>(W1 + offA(c, qy, b), r2);
-          const T bq = bcj[qy], dq = dcj[qy];
+          for (int ks = 0; ks < 4; ++ks) {
+            const int qy = (ks & 1) * 4 + mg;
+            bk[ks] = (ks < nks && mn < ND) ? s_tab[(ks < 2 ? OFF_BR : OFF_DR) + qy * NP + mn] : 0.0;
+          }
+          // k-step outer: the NTL independent accumulators interleave, so no
+          // MFMA waits on the previous one's result
+          bdx_f64x4 acc[NTL];
+          int aoff[NTL];
 #pragma unroll
-          for (int i = 0; i < ND; ++i) c1[i] += bq * r1[i] + dq * r2[i];
+          for (int t = 0; t < NTL; ++t) {
+            const int e = t * 16 + mn < NE ? t * 16 + mn : NE - 1;
+            aoff[t] = offA(c, mg, e / ND) + (e - (e / ND) * ND);
+            acc[t] = bdx_f64x4{0, 0, 0, 0};
+          }
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            if (ks >= nks) break;
+#pragma unroll
+            for (int t = 0; t < NTL; ++t) {
+              const T av = (ks < 2 ? Wk0 : Wk1)[aoff[t] + (ks & 1) * 4 * P1];
+              acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bk[ks], acc[t], 0, 0, 0);
+            }
+          }
+          wave_order();  // every lane's reads are issued before the in-place writes
+          if (mn < ND) {
+#pragma unroll
+            for (int t = 0; t < NTL; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int e = t * 16 + mg + 4 * r;
+                if (e >= NE) continue;
+                const int qz = e / ND, ii = e - (e / ND) * ND;
+                Wout[offA(c, mn, qz) + ii] = acc[t][r];
+              }
+          }
+        };
+        pass(4, W0, W1, W0);
+        if (lane_on) strow<ND>(W1 + offA(c, xa, xb), a3);
+        cell_sync();
+        pass(2, W1, W1, W1);
+        cell_sync();
+      } else {
+        // back y, pass 1: C1 = B_y^T A1 + Dd_y^T A2 -> W0; then A3 -> W1
+        T c1[ND];
+  #pragma unroll
+        for (int i = 0; i < ND; ++i) c1[i] = T(0);
+        if (lane_on && a < ND) {
+          const T* bcj = s_tab + OFF_BC + a * XP;
+          const T* dcj = s_tab + OFF_DC + a * XP;
+  BDX_PRAGMA_UNROLL(2)
+          for (int qy = 0; qy < NQ; ++qy) {
+            T r1[ND], r2[ND];
+            ldrow<ND>(W0 + offA(c, qy, b), r1);
+            ldrow<ND>(W1 + offA(c, qy, b), r2);
+            const T bq = bcj[qy], dq = dcj[qy];
+  #pragma unroll
+            for (int i = 0; i < ND; ++i) c1[i] += bq * r1[i] + dq * r2[i];
+          }
         }
-      }
-      wave_order();
-      if (lane_on && a < ND) strow<ND>(W0 + offA(c, a, b), c1);
-      if (lane_on) strow<ND>(W1 + offA(c, a, b), a3);
-      cell_sync();
-      // pass 2: C3 = B_y^T A3 -> W1
-      T c3[ND];
-#pragma unroll
-      for (int i = 0; i < ND; ++i) c3[i] = T(0);
-      if (lane_on && a < ND) {
-        const T* bcj = s_tab + OFF_BC + a * XP;
-BDX_PRAGMA_UNROLL(2)
-        for (int qy = 0; qy < NQ; ++qy) {
-          T r3[ND];
-          ldrow<ND>(W1 + offA(c, qy, b), r3);
-          const T bq = bcj[qy];
-#pragma unroll
-          for (int i = 0; i < ND; ++i) c3[i] += bq * r3[i];
+        wave_order();
+        if (lane_on && a < ND) strow<ND>(W0 + offA(c, a, b), c1);
+        if (lane_on) strow<ND>(W1 + offA(c, xa, xb), a3);
+        cell_sync();
+        // pass 2: C3 = B_y^T A3 -> W1
+        T c3[ND];
+  #pragma unroll
+        for (int i = 0; i < ND; ++i) c3[i] = T(0);
+        if (lane_on && a < ND) {
+          const T* bcj = s_tab + OFF_BC + a * XP;
+  BDX_PRAGMA_UNROLL(2)
+          for (int qy = 0; qy < NQ; ++qy) {
+            T r3[ND];
+            ldrow<ND>(W1 + offA(c, qy, b), r3);
+            const T bq = bcj[qy];
+  #pragma unroll
+            for (int i = 0; i < ND; ++i) c3[i] += bq * r3[i];
+          }
         }
+        wave_order();
+        if (lane_on && a < ND) strow<ND>(W1 + offA(c, a, b), c3);
+        cell_sync();
       }
-      wave_order();
-      if (lane_on && a < ND) strow<ND>(W1 + offA(c, a, b), c3);
-      cell_sync();
     } else {
       // A3 -> W2 (free since the previous layer's gather); A1, A2 -> W0, W1
       // once every wave finished its front-y reads of them
-      if (lane_on) strow<ND>(W2 + offA(c, a, b), a3);
+      if (lane_on) strow<ND>(W2 + offA(c, xa, xb), a3);
       cell_sync();
       if (lane_on) {
-        strow<ND>(W0 + offA(c, a, b), a1);
-        strow<ND>(W1 + offA(c, a, b), a2);
+        strow<ND>(W0 + offA(c, xa, xb), a1);
+        strow<ND>(W1 + offA(c, xa, xb), a2);
       }
       cell_sync();
       // back y: lanes (c, j = a < ND, qz = b): C1 = B_y^T A1 + Dd_y^T A2, C3 = B_y^T A3
@@ -686,9 +855,60 @@ BDX_PRAGMA_UNROLL(2)
     }
 
     // ------------------------------------------------ back z
-    // lanes (c, j = a < ND, k = b < ND): y_e = B_z^T C1 + Dd_z^T C3
+    if constexpr (MFBZ) {
+      // matrix pipe: y_e[(j, i)][k] = [C1 | C3][(j, i)][(src, qz)] . [B; Dd][(src, qz)][k]
+      // 4 row tiles of 16 (j, i) pairs x 4 k-steps (C1 at qz = g, g + 4, then
+      // C3); the table is the constant B operand (lane: k-row g, column n = z
+      // dof, zero for n >= ND).  Lane (g, n) ends with y_e[(j, i) = 16 t + g + 4 r][k = n].
+      int ltid = tid;
+      asm volatile("" : "+v"(ltid));
+      const int mg = (ltid & 63) >> 4, mn = ltid & 15;
+      double bk[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int qz = (ks & 1) * 4 + mg;
+        bk[ks] = mn < ND ? s_tab[(ks < 2 ? OFF_BR : OFF_DR) + qz * NP + mn] : 0.0;
+      }
+      constexpr int NTL = (ND * ND + 15) / 16;
+      bdx_f64x4 acc[NTL];
+      int aoff[NTL];
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {
+        const int col = t * 16 + mn;
+        const int cc = col < ND * ND ? col : ND * ND - 1;
+        aoff[t] = offA(c, cc / ND, mg) + (cc - (cc / ND) * ND);
+        acc[t] = bdx_f64x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)  // k-step outer: independent accumulators interleave
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) {
+          const T av = (ks < 2 ? W0 : W1)[aoff[t] + (ks & 1) * 4 * RP];
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bk[ks], acc[t], 0, 0, 0);
+        }
+      wave_order();  // every lane's C1 / C3 reads are issued before E overwrites W0
+      if (mn < ND) {
+#pragma unroll
+        for (int t = 0; t < NTL; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int e = t * 16 + mg + 4 * r;
+            if (e >= ND * ND) continue;
+            const int jj = e / ND, ii = e - (e / ND) * ND;
+            const T v = cell_on ? acc[t][r] : T(0);
+            if constexpr (MODE == kFusedCG) {
+              if (!red)
+                pap += static_cast<double>(su[ii * PLP + (ycell + jj) * DZP + zcell + mn]) *
+                       static_cast<double>(v);
+            }
+            W0[offA(c, jj, mn) + ii] = v;
+          }
+      }
+    }
     T ye[ND];
-    if (lane_on && a < ND && b < ND) {
+    if constexpr (MFBZ) {
+    } else if (lane_on && a < ND && b < ND) {
+      // lanes (c, j = a < ND, k = b < ND): y_e = B_z^T C1 + Dd_z^T C3
       const T* bck = s_tab + OFF_BC + b * XP;
       const T* dck = s_tab + OFF_DC + b * XP;
       auto row = [&](int qz, bool first) __attribute__((always_inline)) {
@@ -716,20 +936,22 @@ BDX_PRAGMA_UNROLL(2)
 
     // ------------------------------------------------ element vectors -> A1 of the cell
     const bool dof_lane = cell_on && a < ND && b < ND;
-    if constexpr (MODE == kFusedCG) {
+    if constexpr (MODE == kFusedCG && !MFBZ) {
       if (dof_lane && !red) {
 #pragma unroll
         for (int i = 0; i < ND; ++i)
           pap += static_cast<double>(ua[i * PLP + b]) * static_cast<double>(ye[i]);
       }
     }
-    wave_order();
-    if (lane_on && a < ND && b < ND) {
-      if (!dof_lane) {
+    if constexpr (!MFBZ) {
+      wave_order();
+      if (lane_on && a < ND && b < ND) {
+        if (!dof_lane) {
 #pragma unroll
-        for (int i = 0; i < ND; ++i) ye[i] = T(0);
+          for (int i = 0; i < ND; ++i) ye[i] = T(0);
+        }
+        strow<ND>((WAVELOCAL ? W0 : W2) + offA(c, a, b), ye);
       }
-      strow<ND>((WAVELOCAL ? W0 : W2) + offA(c, a, b), ye);
     }
     __syncthreads();
 

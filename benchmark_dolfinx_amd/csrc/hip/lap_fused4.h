@@ -38,9 +38,6 @@
 
 constexpr int kF4TY = 4, kF4TZ = 4;  // cell tile
 
-typedef double bdx_f64x4 __attribute__((ext_vector_type(4)));
-typedef double bdx_f64x2 __attribute__((ext_vector_type(2)));
-
 // kernarg table layout: M1, K1, C1 (4 x 4 row-major each)
 constexpr int kF4Tab = 48;
 

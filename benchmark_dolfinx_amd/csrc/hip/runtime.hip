@@ -1014,10 +1014,11 @@ struct CGRuntime final : LoopBase {
     std::vector<double> v[5];
     bdx::Watchdog::Busy busy(t.watchdog());
     for (int it = 0; it < reps; ++it) {
-      // alone: the chain, the interior, one exchange
+      // alone: the chain, the interior, one exchange (each drained before the next)
       BDX_CHECK(hipEventRecord(e[0], cs));
       if ((rc = chain(cs))) return rc;
       BDX_CHECK(hipEventRecord(e[1], cs));
+      BDX_CHECK(hipDeviceSynchronize());
       BDX_CHECK(hipEventRecord(e[2], st));
       if ((rc = launch_op(0, true, false, kXSingle, ra, st))) return rc;
       BDX_CHECK(hipEventRecord(e[3], st));

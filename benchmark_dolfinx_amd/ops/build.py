@@ -97,6 +97,9 @@ def build_host(force: bool = False, sanitize: bool = False) -> Path:
 def hip_flags(csrc: Path = CSRC) -> list[str]:
     return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={HIP_ARCH}",
             "-munsafe-fp-atomics", "-ffp-contract=fast", "-Wno-unused-result",
+            # MFMA accumulators in VGPRs (unified register file): the AGPR form
+            # pushed the Q6 fused3 CG instance over 256 registers (1 wave / SIMD)
+            "-mllvm", "-amdgpu-mfma-vgpr-form",
             "-I", str(csrc / "include"), "-I", str(csrc / "hip")]
 
 

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Interleaved same-box A/B of variant libraries against the production build.
-#   bash scripts/r3_ab.sh "<bench args>" variant1 [variant2 ...]
+#   [AB_REPS=n] bash scripts/ab.sh "<bench args>" variant1 [variant2 ...]
 # (variant = NAME of benchmark_dolfinx_amd/ops/libbdx_hip_NAME.so, or "prod")
 source scripts/gpu_steps.sh
 args=$1; shift
 tag=$(echo "$args" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   for v in prod "$@"; do
     if [ "$v" = prod ]; then
       step ab_${tag}_${v}_$rep 300 python -u bench.py $args
