@@ -985,19 +985,21 @@ struct CGRuntime final : LoopBase {
     };
     const int iy = cfg.nty - 1, iz = cfg.ntz - 1;
     const int ra[4] = {0, iy, 0, iz}, r1[4] = {iy, cfg.nty, 0, cfg.ntz}, r2[4] = {0, iy, iz, cfg.ntz};
-    auto chain = [&](hipStream_t s) {
+    // ev (optional): recorded when the forward exchange is done
+    auto chain = [&](hipStream_t s, hipEvent_t ev = nullptr) {
       int rc = xchg(s);
+      if (!rc && ev) rc = static_cast<int>(hipEventRecord(ev, s));
       if (!rc) rc = launch_op(0, true, false, kXSingle, r1, s);
       if (!rc) rc = launch_op(0, true, false, kXSingle, r2, s);
       if (!rc) rc = xchg(s);
       return rc;
     };
-    hipEvent_t e[4] = {};
+    hipEvent_t e[5] = {};
     for (auto& x : e) BDX_CHECK(hipEventCreate(&x));
     struct Free {
       hipEvent_t* e;
       ~Free() {
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 5; ++i)
           if (e[i]) hipEventDestroy(e[i]);
       }
     } fr{e};
@@ -1011,7 +1013,7 @@ struct CGRuntime final : LoopBase {
     if (!rc) rc = launch_op(0, true, false, kXSingle, ra, st);
     if (rc) return rc;
     BDX_CHECK(hipDeviceSynchronize());
-    std::vector<double> v[5];
+    std::vector<double> v[6];
     bdx::Watchdog::Busy busy(t.watchdog());
     for (int it = 0; it < reps; ++it) {
       // alone: the chain, the interior, one exchange (each drained before the next)
@@ -1033,15 +1035,16 @@ struct CGRuntime final : LoopBase {
       // together, enqueued in the runtime's order: fork, cs chain, st interior
       BDX_CHECK(hipEventRecord(e[0], st));
       BDX_CHECK(hipStreamWaitEvent(cs, e[0], 0));
-      if ((rc = chain(cs))) return rc;
+      if ((rc = chain(cs, e[4]))) return rc;
       BDX_CHECK(hipEventRecord(e[1], cs));
       if ((rc = launch_op(0, true, false, kXSingle, ra, st))) return rc;
       BDX_CHECK(hipEventRecord(e[2], st));
       BDX_CHECK(hipDeviceSynchronize());
       v[2].push_back(ms(0, 1));
       v[3].push_back(ms(0, 2));
+      v[5].push_back(ms(0, 4));
     }
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < 6; ++i) {
       std::sort(v[i].begin(), v[i].end());
       out[i] = v[i][v[i].size() / 2];
     }
@@ -1421,7 +1424,7 @@ int bdx_rt_preflight(void* h, double timeout_s, double* out) {
 }
 
 // Comm/compute overlap probe on one GPU (see CGRuntime::overlap_probe;
-// fused operators only); buf: 2 n doubles; out[5].
+// fused operators only); buf: 2 n doubles; out[6].
 int bdx_rt_overlap_probe(void* h, int64_t n, double* buf, int reps, double* out) {
   return with_rt(h, [&](LoopBase* rt) -> int {
     if (auto* f = dynamic_cast<CGRuntime<double>*>(rt)) return f->overlap_probe(n, buf, reps, out);

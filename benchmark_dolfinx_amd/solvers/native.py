@@ -220,14 +220,14 @@ class NativeCGRuntime:
         CG state (restart CG afterwards)."""
         buf = torch.zeros(2 * int(n), dtype=torch.float64, device=self.pb.device)
         buf[:n] = torch.arange(n, dtype=torch.float64, device=self.pb.device)
-        out = (ctypes.c_double * 5)()
+        out = (ctypes.c_double * 6)()
         torch.cuda.synchronize()
         _check(self.lib.bdx_rt_overlap_probe(self.h, int(n), ptr(buf), int(reps), out),
                "rt_overlap_probe")
         torch.cuda.synchronize()
         ok = bool(torch.equal(buf[n:], buf[:n]))
         keys = ("chain_alone_ms", "interior_alone_ms", "chain_done_ms", "interior_done_ms",
-                "exchange_alone_ms")
+                "exchange_alone_ms", "fwd_exchange_done_ms")
         rec = {k: float(v) for k, v in zip(keys, out)}
         rec["exchange_ok"] = ok
         rec["bytes"] = int(n) * 8
