@@ -139,6 +139,87 @@ __global__ void __launch_bounds__(NT) march_kernel(Geo g, int work, const double
   (void)pin_bytes;
 }
 
+// The same traffic with 16-byte accesses wherever a tile row allows: the 12
+// own nodes of a row as 6 pairs, the neighbour's 13th column element and the
+// corner as single loads; writes of own nodes as pairs.
+__global__ void __launch_bounds__(NT) march_vec_kernel(Geo g, int work, const double* __restrict__ r,
+                                                      const double* __restrict__ p, double* __restrict__ pn,
+                                                      double* __restrict__ y, double* sink) {
+  typedef double V __attribute__((ext_vector_type(2)));
+  extern __shared__ double lds[];
+  const int tile = blockIdx.x;
+  const int ty = tile / g.ntz, tz = tile % g.ntz;
+  const int tid = threadIdx.x;
+  // load items per plane: 13 rows x 6 pairs (row 12 from the y neighbour) +
+  // 13 singles (column 12 from the z neighbour, incl. the corner) = 91
+  constexpr int NIT = 13 * 6 + 13, NLI = (P * NIT + NT - 1) / NT;
+  long lo[NLI];
+  int lk[NLI];  // 0 none, 1 pair, 2 single
+#pragma unroll
+  for (int k = 0; k < NLI; ++k) {
+    const int e = tid + k * NT;
+    lk[k] = 0;
+    lo[k] = 0;
+    if (e < P * NIT) {
+      const int pl = e / NIT, it = e % NIT;
+      int ly, lz, tyy = ty, tzz = tz;
+      if (it < 78) { ly = it / 6; lz = 2 * (it % 6); lk[k] = 1; }
+      else { ly = it - 78; lz = 0; ++tzz; lk[k] = 2; }
+      if (ly == TP) { ly = 0; ++tyy; }
+      if (tyy >= g.nty || tzz >= g.ntz) lk[k] = 0;
+      lo[k] = lk[k] ? toff(g, tyy, tzz, pl, ly, lz) : 0;
+    }
+  }
+  constexpr int NSI = (P * 72 + NT - 1) / NT;  // own pairs per layer
+  long so[NSI];
+  bool son[NSI];
+#pragma unroll
+  for (int k = 0; k < NSI; ++k) {
+    const int e = tid + k * NT;
+    son[k] = e < P * 72;
+    const int pl = son[k] ? e / 72 : 0, it = e % 72;
+    so[k] = son[k] ? toff(g, ty, tz, pl, it / 6, 2 * (it % 6)) : 0;
+  }
+  const long lstep = static_cast<long>(P) * TP * TP;
+  const int nlay = g.X / P;
+  double acc = 0.0;
+  V vr[NLI], vp[NLI];
+  auto issue = [&](int cx) {
+#pragma unroll
+    for (int k = 0; k < NLI; ++k) {
+      const long o = lo[k] + static_cast<long>(cx) * lstep;
+      vr[k] = V{0, 0};
+      vp[k] = V{0, 0};
+      if (cx < nlay && lk[k] == 1) {
+        vr[k] = __builtin_nontemporal_load(reinterpret_cast<const V*>(r + o));
+        vp[k] = __builtin_nontemporal_load(reinterpret_cast<const V*>(p + o));
+      } else if (cx < nlay && lk[k] == 2) {
+        vr[k][0] = __builtin_nontemporal_load(r + o);
+        vp[k][0] = __builtin_nontemporal_load(p + o);
+      }
+    }
+  };
+  issue(0);
+  for (int cx = 0; cx < nlay; ++cx) {
+    const double c = burn(static_cast<double>(cx + tid), work);
+    double sacc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NLI; ++k) sacc += vr[k][0] + vr[k][1] + 0.5 * (vp[k][0] + vp[k][1]);
+    lds[tid] = sacc;
+#pragma unroll
+    for (int k = 0; k < NSI; ++k) {
+      const long o = so[k] + static_cast<long>(cx) * lstep;
+      if (son[k]) {
+        *reinterpret_cast<V*>(pn + o) = V{sacc + k, sacc};
+        *reinterpret_cast<V*>(y + o) = V{c + k, c};
+      }
+    }
+    acc += c;
+    issue(cx + 1);
+  }
+  if (acc == 12345.678) sink[0] = acc + lds[tid];
+}
+
 int main(int argc, char** argv) {
   // 1024 tiles = one round at 4 workgroups per CU on 256 CUs; ~300 M doubles
   Geo g;
@@ -160,14 +241,16 @@ int main(int argc, char** argv) {
   const double bytes = 8.0 * n * (2.0 * 169.0 / 144.0 + 2.0);  // patch reads + own writes
   std::printf("n = %ld doubles, LDS pin %d B, %d tiles\n", n, pin, g.nty * g.ntz);
   for (int work : {0, 2, 4, 8, 12, 16}) {
-    for (int depth = 1; depth <= 2; ++depth) {
+    for (int depth = 1; depth <= 3; ++depth) {  // 3: depth 1 with 16-byte accesses
       float best = 1e30f;
       for (int rep = 0; rep < 4; ++rep) {
         CK(hipEventRecord(t0));
         if (depth == 1)
           march_kernel<1><<<g.nty * g.ntz, NT, pin>>>(g, work, r, p, pn, y, sink, pin);
-        else
+        else if (depth == 2)
           march_kernel<2><<<g.nty * g.ntz, NT, pin>>>(g, work, r, p, pn, y, sink, pin);
+        else
+          march_vec_kernel<<<g.nty * g.ntz, NT, pin>>>(g, work, r, p, pn, y, sink);
         CK(hipGetLastError());
         CK(hipEventRecord(t1));
         CK(hipEventSynchronize(t1));
@@ -175,8 +258,8 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, t0, t1));
         if (rep > 0 && ms < best) best = ms;
       }
-      std::printf("work %2d depth %d: %8.3f ms  %6.2f TB/s (patch-read + own-write bytes)\n", work,
-                  depth, best, bytes / (best * 1e-3) / 1e12);
+      std::printf("work %2d %s: %8.3f ms  %6.2f TB/s (patch-read + own-write bytes)\n", work,
+                  depth == 1 ? "depth 1      " : depth == 2 ? "depth 2      " : "depth 1, 16 B", best, bytes / (best * 1e-3) / 1e12);
     }
   }
   return 0;
