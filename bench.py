@@ -73,8 +73,8 @@ def parse_args(argv=None):
     ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
                     help="after the headline, time variants of it: the perturbed "
                          "(general trilinear) mesh, the "
-                         "reference's data model (dofmap + stored G) and Q6 perturbed "
-                         "(GPU only; auto: on for one rank)")
+                         "reference's data model (dofmap + stored G, Q3 and Q6) and Q6 "
+                         "perturbed (GPU only; auto: on for one rank)")
     return ap.parse_args(argv)
 
 
@@ -338,7 +338,9 @@ def run(comm, a) -> dict | None:
                                                       geometry="otf-general")),
                  ("dofmap", a.config, dict(kappa=a.kappa, perturb=a.perturb, kernel="dofmap",
                                            geometry="stored")),
-                 ("q6_general", "q6", dict(kappa=a.kappa, perturb=pert)))
+                 ("q6_general", "q6", dict(kappa=a.kappa, perturb=pert)),
+                 ("q6_dofmap", "q6", dict(kappa=a.kappa, perturb=a.perturb, kernel="dofmap",
+                                          geometry="stored")))
         for key, cfg, kw in specs:
             if cfg != a.config and (a.mesh or a.config != "q3"):
                 continue
@@ -403,6 +405,7 @@ def _record(a, n, head, companions, extras, flags, gpu) -> dict:
         "general_trilinear_gdofs": extras.get("general_trilinear", {}).get("value"),
         "dofmap_gdofs": extras.get("dofmap", {}).get("value"),
         "q6_general_gdofs": extras.get("q6_general", {}).get("value"),
+        "q6_dofmap_gdofs": extras.get("q6_dofmap", {}).get("value"),
         "variants": extras,
     }
 
