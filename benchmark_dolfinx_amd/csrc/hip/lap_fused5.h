@@ -48,6 +48,9 @@
 // measured 9 % slower (profiles/r2_launder.md).
 constexpr int kF5Waves = 2;
 
+// 16-byte staging loads / stores (the VEC instance, lap_fused5_kernel)
+constexpr bool kF5Vec = true;
+
 // table layout: M, K, C, C^T as 8 x 8 row-major blocks, then the even-odd
 // forms of M and K (4 x 4 blocks at kF5EO + 32 id: E, then O at + 16)
 constexpr int kF5Stride = 8;
@@ -106,10 +109,18 @@ struct F5Shape {
   static constexpr int DZP = DZ | 1, PLP = DY * DZP;
 };
 
+// Does a tile row's own part split into whole 16-byte vectors (the VEC instance)?
+template <typename T, int ND>
+constexpr bool f5_vec_shape() {
+  using S = F5Shape<T, ND, 2>;
+  constexpr int V = 16 / static_cast<int>(sizeof(T)), OWNZ = S::TZ * S::P;
+  return kF5Vec && OWNZ % V == 0 && (OWNZ * static_cast<int>(sizeof(T))) % 16 == 0;
+}
+
 // fused5: nodal x / z / y Kronecker passes for parallelepiped cells, P = 3..7.
 // (An MFMA form of the three passes lost to this VALU core at Q6 in both
 // precisions: profiles/r2_fused5_mfma.md, profiles/r3_mfma.md.)
-template <typename T, int ND, int NARR, int MODE>
+template <typename T, int ND, int NARR, int MODE, bool VEC = false>
 __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
     lap_fused5_kernel(Fused2Args<T> A, const T* __restrict__ tabd) {
   using S = F5Shape<T, ND, NARR>;
@@ -118,6 +129,19 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
   constexpr int NT = S::NT, ND2 = ND * ND, NDP = S::NDP, ARR = S::ARR, WB = S::WB;
   constexpr int RP = S::RP, P1 = S::P1, PC = S::PC;
   constexpr bool MIXED = NARR == 4;
+  // VEC: the next layer's loads and the staging's p / x stores move 16 bytes
+  // per lane -- items of V consecutive z-nodes of a tile row (its OWNZ own
+  // nodes) plus one single node (the z-neighbour's first column); the host
+  // selects this instance only when every row of a tile is 16-byte aligned
+  // (launch_fused5)
+  constexpr int V = 16 / static_cast<int>(sizeof(T));
+  constexpr int OWNZ = TZ * P;
+  static_assert(!VEC || (OWNZ % V == 0 && (OWNZ * static_cast<int>(sizeof(T))) % 16 == 0),
+                "VEC: whole 16-byte vectors per tile row");
+  constexpr int NIV = OWNZ / V;
+  constexpr int NITV = P * DY * NIV, NPI = VEC ? (NITV + NT - 1) / NT : 1;  // vector items
+  constexpr int NITS = P * DY, NPS = VEC ? (NITS + NT - 1) / NT : 1;         // single items
+  typedef T VT __attribute__((ext_vector_type(V)));
   constexpr int NPF = (P * PL + NT - 1) / NT;
   constexpr int NOUT = (ND * PL + NT - 1) / NT;
   constexpr int NCP = (PL + NT - 1) / NT;
@@ -129,7 +153,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
   static_assert(ND * PLP < (1 << 23), "staging offset field");
 
   __shared__ __attribute__((aligned(16))) T s_w[ZSLOT + 1];
-  __shared__ T s_u[2][ND * PLP];
+  __shared__ T s_u[2][ND * PLP + V];  // + dummy slots (VEC padding items)
   __shared__ T s_c[2][PL];
   __shared__ T s_X[2][2 * NV];
   __shared__ double s_red[16];
@@ -247,6 +271,47 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
       st_goff[k] = static_cast<unsigned>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz));
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
+  }
+  // ---- VEC: per-thread staging items (planes 1..P).  Vector item = (plane,
+  // tile row ly, iz < NIV): the V own nodes lz = V iz .. V iz + V - 1; single
+  // item = (plane, ly): the node lz = OWNZ (the z-neighbour's first column).
+  // meta: 4 flag bits per node (kValid, kOwnT, kBcYZ, kRownYZ) at 4 e, the
+  // plane at bits 16-19, any node valid at 21, every node owned at 22, any
+  // node owned at 23
+  unsigned it_goff[NPI], is_goff[NPS];
+  int it_meta[NPI], it_lds[NPI], is_meta[NPS], is_lds[NPS];
+  auto item_desc = [&](int pl, int ly, int lz0, int nel, unsigned& goff, int& meta, int& lds) {
+    int m = pl << 16, allown = 1, anyown = 0, anyv = 0;
+    for (int e = 0; e < nel; ++e) {
+      const int f = yz_flags(ly, lz0 + e);
+      m |= f << (4 * e);
+      anyv |= f & kValid;
+      allown &= (f & kOwnT) ? 1 : 0;
+      anyown |= (f & kOwnT) ? 1 : 0;
+    }
+    meta = m | (anyv ? 1 << 21 : 0) | (allown ? 1 << 22 : 0) | (anyown ? 1 << 23 : 0);
+    goff = anyv ? static_cast<unsigned>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz0)) : 0u;
+    lds = pl * PLP + ly * DZP + lz0;
+  };
+#pragma unroll
+  for (int k = 0; k < NPI; ++k) {
+    it_goff[k] = 0;
+    it_meta[k] = 0;
+    it_lds[k] = ND * PLP;  // padding items: the dummy LDS slots
+    const int it = tid + k * NT;
+    if (VEC && it < NITV) {
+      const int pl = 1 + it / (DY * NIV), rem = it % (DY * NIV);
+      item_desc(pl, rem / NIV, (rem % NIV) * V, V, it_goff[k], it_meta[k], it_lds[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NPS; ++k) {
+    is_goff[k] = 0;
+    is_meta[k] = 0;
+    is_lds[k] = ND * PLP;
+    const int it = tid + k * NT;
+    if (VEC && it < NITS)
+      item_desc(1 + it / DY, it % DY, OWNZ, 1, is_goff[k], is_meta[k], is_lds[k]);
   }
   // ---- per-thread output descriptors (planes 0..P of a layer)
   int o_src[NOUT][2], o_off[NOUT], o_meta[NOUT];
@@ -426,14 +491,44 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
     const T* __restrict__ un_p = A.pold + lnext;
     T* __restrict__ un_x = A.x + lnext;
     const T* un_q = A.pnew + lnext;  // p_prev2 (kXPair), read before the staging store
-    T pf_r[NPF], pf_p[NPF], pf_x[NPF], pf_q[NPF];
+    T pf_r[VEC ? 1 : NPF], pf_p[VEC ? 1 : NPF], pf_x[VEC ? 1 : NPF], pf_q[VEC ? 1 : NPF];
+    VT vf_r[NPI], vf_p[NPI], vf_x[NPI], vf_q[NPI];
+    T sf_r[NPS], sf_p[NPS], sf_x[NPS], sf_q[NPS];
     T pf_v[NPV];
     // next layer's cell coefficient rides with the prefetch: a load consumed
     // in the same layer would make the wave wait for the whole batch
     T kc_nxt = kc_cur;
     if (A.kc && !last && cell_on) kc_nxt = A.kc[static_cast<int64_t>(cx + 1) * kc_ps + kc_cell];
 #pragma unroll
-    for (int k = 0; k < NPF; ++k) {
+    for (int k = 0; k < NPI; ++k) {
+      vf_r[k] = vf_p[k] = vf_x[k] = vf_q[k] = VT{};
+      if constexpr (VEC) {
+        const int m = it_meta[k];
+        if (last || !(m & (1 << 21))) continue;
+        vf_r[k] = *reinterpret_cast<const VT*>(un_r + it_goff[k]);
+        if constexpr (MODE == kFusedCG) {
+          vf_p[k] = *reinterpret_cast<const VT*>(un_p + it_goff[k]);
+          if (xupd && (m & (1 << 23))) vf_x[k] = *reinterpret_cast<const VT*>(un_x + it_goff[k]);
+          if (xpair && (m & (1 << 23))) vf_q[k] = *reinterpret_cast<const VT*>(un_q + it_goff[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPS; ++k) {
+      sf_r[k] = sf_p[k] = sf_x[k] = sf_q[k] = T(0);
+      if constexpr (VEC) {
+        const int m = is_meta[k];
+        if (last || !(m & (1 << 21))) continue;
+        sf_r[k] = ld_stream(un_r + is_goff[k]);
+        if constexpr (MODE == kFusedCG) {
+          sf_p[k] = ld_stream(un_p + is_goff[k]);
+          if (xupd && (m & (1 << 23))) sf_x[k] = ld_stream(un_x + is_goff[k]);
+          if (xpair && (m & (1 << 23))) sf_q[k] = ld_stream(un_q + is_goff[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < (VEC ? 0 : NPF); ++k) {
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
@@ -667,6 +762,95 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
       }
 
     };
+    auto do_stage_vec = [&]() __attribute__((always_inline)) {
+      // ------------------------------------------------ stage the next layer (VEC items)
+      if (!last) {
+#pragma unroll
+        for (int k = 0; k < NPI; ++k)
+          asm volatile("" : "+v"(it_goff[k]), "+v"(it_meta[k]), "+v"(it_lds[k]));
+#pragma unroll
+        for (int k = 0; k < NPS; ++k)
+          asm volatile("" : "+v"(is_goff[k]), "+v"(is_meta[k]), "+v"(is_lds[k]));
+        T* __restrict__ un = s_u[nxt];
+#pragma unroll
+        for (int k = 0; k < NCP; ++k)
+          if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
+        T* __restrict__ pnl = A.pnew + lnext;
+        T* __restrict__ yl = A.y + lnext;
+        // node e of an item: Dirichlet identity row (plane 0 of the march is
+        // the prologue's); returns the value staged into LDS
+        auto dirichlet = [&](int m, int e, unsigned goff, T v) __attribute__((always_inline)) -> T {
+          const int f = (m >> (4 * e)) & 15;
+          const int gxx = (cx + 1) * P + ((m >> 16) & 15);
+          if (!(f & kValid)) return T(0);
+          if ((f & kBcYZ) || gxx == A.bcx_hi) {
+            if (f & kOwnT) {
+              const bool rown = (f & kRownYZ) && gxx < A.ownx;
+              yl[goff + e] = rown ? v : T(0);
+              if constexpr (MODE == kFusedCG) {
+                if (rown) pap += static_cast<double>(v) * static_cast<double>(v);
+              }
+            }
+            return T(0);
+          }
+          return v;
+        };
+#pragma unroll
+        for (int k = 0; k < NPI; ++k) {
+          const int m = it_meta[k];
+          VT val;
+          if constexpr (MODE == kFusedCG) {
+            val = vf_r[k] + beta * vf_p[k];
+            VT xn = vf_x[k] + xalpha * vf_p[k];
+            if (xpair) xn += xalpha2 * vf_q[k];
+            if (m & (1 << 22)) {  // every node owned: whole vectors
+              *reinterpret_cast<VT*>(pnl + it_goff[k]) = val;
+              if (xupd) *reinterpret_cast<VT*>(un_x + it_goff[k]) = xn;
+            } else if (m & (1 << 23)) {  // some owned (a tile at the domain's edge)
+#pragma unroll
+              for (int e = 0; e < V; ++e) {
+                if (!((m >> (4 * e)) & kOwnT)) continue;
+                pnl[it_goff[k] + e] = val[e];
+                if (xupd) un_x[it_goff[k] + e] = xn[e];
+              }
+            }
+          } else {
+            val = vf_r[k];
+          }
+#pragma unroll
+          for (int e = 0; e < V; ++e) un[it_lds[k] + e] = dirichlet(m, e, it_goff[k], val[e]);
+        }
+#pragma unroll
+        for (int k = 0; k < NPS; ++k) {
+          const int m = is_meta[k];
+          T val;
+          if constexpr (MODE == kFusedCG) {
+            val = sf_r[k] + beta * sf_p[k];
+            if (m & (1 << 23)) {
+              pnl[is_goff[k]] = val;
+              if (xupd) {
+                T xn = sf_x[k] + xalpha * sf_p[k];
+                if (xpair) xn += xalpha2 * sf_q[k];
+                un_x[is_goff[k]] = xn;
+              }
+            }
+          } else {
+            val = sf_r[k];
+          }
+          if (tid + k * NT < NITS) un[is_lds[k]] = dirichlet(m, 0, is_goff[k], val);
+        }
+#pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][e] = sX[NV + e];
+        }
+#pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][NV + e] = pf_v[k];
+        }
+      }
+    };
     auto do_stage = [&]() __attribute__((always_inline)) {
       // ------------------------------------------------ stage the next layer
       if (!last) {
@@ -738,7 +922,10 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
     // pass sees nothing outstanding and does not put a draining wait before
     // each slot's stores.
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    do_stage();
+    if constexpr (VEC)
+      do_stage_vec();
+    else
+      do_stage();
     do_gather();
     kc_cur = kc_nxt;
   }
@@ -802,10 +989,33 @@ inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, co
 
 // affine_ok: 0 = general cells (refused), 1 = parallelepipeds, 2 = axis-aligned
 // boxes (diagonal Jacobians: the 2-array instance)
+// Can the VEC instance run on this launch?  Every tile row's own nodes must
+// start on a 16-byte boundary: the tiled storage's tiles are the kernel's
+// (y, z) tiles, or the lattice rows are padded to whole vectors, and the
+// vectors themselves are 16-byte aligned.
+template <typename T, int ND>
+bool f5_vec_ok(const Fused2Args<T>& a) {
+  using S = F5Shape<T, ND, 2>;
+  constexpr int V = 16 / static_cast<int>(sizeof(T)), OWNZ = S::TZ * S::P;
+  if (OWNZ % V || (OWNZ * static_cast<int>(sizeof(T))) % 16) return false;
+  // lattice layout: the padded row pitch holds every tile's vectors (the top
+  // tile's run past the domain but not past the row)
+  const bool lay = a.tsy ? (a.tsy == S::TY * S::P && a.tsz == OWNZ)
+                         : (a.ld % V == 0 && a.ps % V == 0 && static_cast<int64_t>(a.ntz) * OWNZ <= a.ld);
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return lay && al(a.u) && al(a.pold) && al(a.pnew) && al(a.x);
+}
+
 template <typename T, int ND, int MODE>
 int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStream_t st) {
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
+  if constexpr (MODE == kFusedCG && f5_vec_shape<T, ND>()) {
+    if (affine_ok == 2 && f5_vec_ok<T, ND>(a)) {
+      lap_fused5_kernel<T, ND, 2, MODE, true><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   if (affine_ok == 2)
     lap_fused5_kernel<T, ND, 2, MODE><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
   else
@@ -864,7 +1074,8 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     if (e == hipSuccess)                                                           \
       e = affine_ok == 2                                                           \
               ? hipOccupancyMaxActiveBlocksPerMultiprocessor(                      \
-                    &per_cu, lap_fused5_kernel<T, PP + 1, 2, kFusedCG>,            \
+                    &per_cu, lap_fused5_kernel<T, PP + 1, 2, kFusedCG,             \
+                                               f5_vec_shape<T, PP + 1>()>,             \
                     F5Shape<T, PP + 1, 2>::NT, 0)                                  \
               : hipOccupancyMaxActiveBlocksPerMultiprocessor(                      \
                     &per_cu, lap_fused5_kernel<T, PP + 1, 4, kFusedCG>,            \
