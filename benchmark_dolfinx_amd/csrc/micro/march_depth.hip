@@ -55,6 +55,7 @@ __device__ __forceinline__ double burn(double v, int work) {
   return a0 + a1 + a2 + a3;
 }
 
+// The operator's traffic per layer with DEPTH layers of loads in flight.
 template <int DEPTH>
 __global__ void __launch_bounds__(NT) march_kernel(Geo g, int work, const double* __restrict__ r,
                                                    const double* __restrict__ p, double* __restrict__ pn,
@@ -259,7 +260,8 @@ int main(int argc, char** argv) {
         if (rep > 0 && ms < best) best = ms;
       }
       std::printf("work %2d %s: %8.3f ms  %6.2f TB/s (patch-read + own-write bytes)\n", work,
-                  depth == 1 ? "depth 1      " : depth == 2 ? "depth 2      " : "depth 1, 16 B", best, bytes / (best * 1e-3) / 1e12);
+                  depth == 1 ? "depth 1      " : depth == 2 ? "depth 2      " : "depth 1, 16 B", best,
+                  bytes / (best * 1e-3) / 1e12);
     }
   }
   return 0;
