@@ -55,13 +55,16 @@ template <int NQ, int AFF> struct Fused3Waves {
 // + back z 30.9 (adopted); all four 30.2 (the front-y stage's lane exchange
 // stalls on its MFMA results).
 constexpr bool kF3MfmaFrontZ = true;
+// 16-byte staging loads / stores (the VEC instance, as lap_fused5.h)
+constexpr bool kF3Vec = true;
 constexpr bool kF3MfmaFrontY = false;
 constexpr bool kF3MfmaBackY = true;
 constexpr bool kF3MfmaBackZ = true;
 
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
-template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF>
-__global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fused3Waves<NQ, AFF>::value))
+template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF, bool VEC = false>
+__global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads),
+                                  (VEC && NQ == 8 && sizeof(T) == 8 ? 2 : Fused3Waves<NQ, AFF>::value))
     lap_fused3_kernel(Fused2Args<T> A, FusedTables<T> tb) {
   using S = FusedShape<T, ND, NQ, TY, TZ>;
   constexpr int P = S::P, DY = S::DY, DZ = S::DZ, PL = DY * DZ;
@@ -75,6 +78,17 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
   constexpr int NV = (TY + 1) * (TZ + 1) * 3;
   constexpr int NPV = (NV + NT - 1) / NT;
   constexpr int XP = S::XP, NP = S::NP;
+  // VEC: the staging's loads and p / x stores in 16-byte vectors (items of V
+  // z-nodes of a tile row, the z-neighbour's column as single items), as in
+  // lap_fused5.h; the host selects it when every tile row is 16-byte aligned
+  constexpr int V = 16 / static_cast<int>(sizeof(T));
+  constexpr int OWNZ = TZ * P;
+  static_assert(!VEC || (OWNZ % V == 0 && (OWNZ * static_cast<int>(sizeof(T))) % 16 == 0),
+                "VEC: whole 16-byte vectors per tile row");
+  constexpr int NIV = OWNZ / V;
+  constexpr int NITV = P * DY * NIV, NPI = VEC ? (NITV + NT - 1) / NT : 1;
+  constexpr int NITS = P * DY, NPS = VEC ? (NITS + NT - 1) / NT : 1;
+  typedef T VT __attribute__((ext_vector_type(V)));
   // intra-cell stages only exchange data inside a wave when a cell's NQ^2
   // columns tile whole waves
   constexpr bool WAVELOCAL = (64 % NQ2 == 0) && (S::lanes % 64 == 0);
@@ -116,7 +130,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
 
   __shared__ __attribute__((aligned(16))) T s_tab[TAB3];
   __shared__ T s_qw[2 * NQ];
-  __shared__ T s_u[2][ND * PLP];
+  __shared__ T s_u[2][ND * PLP + V];  // + dummy slots (VEC padding items)
   __shared__ T s_c[2][PL];
   __shared__ __attribute__((aligned(16))) T s_wa[NBUFS * NWBUF + RP];
   __shared__ T s_X[2][2 * NV];
@@ -224,6 +238,43 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
       st_goff[k] = static_cast<int>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz));
       st_meta[k] = f | (pl << 4) | ((pl * PLP + ly * DZP + lz) << 8);
     }
+  }
+  // ---- VEC staging items (lap_fused5.h): meta = 4 flag bits per node at
+  // 4 e, the plane at bits 16-19, any node valid at 21, every node owned at
+  // 22, any node owned at 23
+  unsigned it_goff[NPI], is_goff[NPS];
+  int it_meta[NPI], it_lds[NPI], is_meta[NPS], is_lds[NPS];
+  auto item_desc = [&](int pl, int ly, int lz0, int nel, unsigned& goff, int& meta, int& lds) {
+    int m = pl << 16, allown = 1, anyown = 0, anyv = 0;
+    for (int e = 0; e < nel; ++e) {
+      const int f = yz_flags(ly, lz0 + e);
+      m |= f << (4 * e);
+      anyv |= f & kValid;
+      allown &= (f & kOwnT) ? 1 : 0;
+      anyown |= (f & kOwnT) ? 1 : 0;
+    }
+    meta = m | (anyv ? 1 << 21 : 0) | (allown ? 1 << 22 : 0) | (anyown ? 1 << 23 : 0);
+    goff = anyv ? static_cast<unsigned>(pl * A.ps + fused_yzoff(A, y0 + ly, z0 + lz0)) : 0u;
+    lds = pl * PLP + ly * DZP + lz0;
+  };
+#pragma unroll
+  for (int k = 0; k < NPI; ++k) {
+    it_goff[k] = 0;
+    it_meta[k] = 0;
+    it_lds[k] = ND * PLP;  // padding items: the dummy LDS slots
+    const int it = tid + k * NT;
+    if (VEC && it < NITV) {
+      const int pl = 1 + it / (DY * NIV), rem = it % (DY * NIV);
+      item_desc(pl, rem / NIV, (rem % NIV) * V, V, it_goff[k], it_meta[k], it_lds[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NPS; ++k) {
+    is_goff[k] = 0;
+    is_meta[k] = 0;
+    is_lds[k] = ND * PLP;
+    const int it = tid + k * NT;
+    if (VEC && it < NITS) item_desc(1 + it / DY, it % DY, OWNZ, 1, is_goff[k], is_meta[k], is_lds[k]);
   }
   // ---- per-thread output descriptors (planes 0..P of a layer): slot e's
   // <= 4 LDS sources (packed 16-bit pairs), destination offset and meta
@@ -350,7 +401,9 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
 
     // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
     const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
-    T pf_r[NPF], pf_p[NPF], pf_x[NPF];
+    T pf_r[VEC ? 1 : NPF], pf_p[VEC ? 1 : NPF], pf_x[VEC ? 1 : NPF];
+    VT vf_r[NPI], vf_p[NPI], vf_x[NPI];
+    T sf_r[NPS], sf_p[NPS], sf_x[NPS];
     T pf_v[NPV];
     // vertex plane and coefficient first: the loads whose addresses may come
     // back from a register spill (and its vmcnt wait) go before the vector
@@ -362,8 +415,37 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), (Fus
       pf_v[k] = T(0);
       if (!last && v_off[k] >= 0) pf_v[k] = A.xv[static_cast<int64_t>(cx + 2) * A.vps + v_off[k]];
     }
+    const T* __restrict__ un_r = A.u + lnext;
+    const T* __restrict__ un_p = A.pold + lnext;
+    T* __restrict__ un_x = A.x + lnext;
 #pragma unroll
-    for (int k = 0; k < NPF; ++k) {
+    for (int k = 0; k < NPI; ++k) {
+      vf_r[k] = vf_p[k] = vf_x[k] = VT{};
+      if constexpr (VEC) {
+        const int m = it_meta[k];
+        if (last || !(m & (1 << 21))) continue;
+        vf_r[k] = *reinterpret_cast<const VT*>(un_r + it_goff[k]);
+        if constexpr (MODE == kFusedCG) {
+          vf_p[k] = *reinterpret_cast<const VT*>(un_p + it_goff[k]);
+          if (xupd && (m & (1 << 23))) vf_x[k] = *reinterpret_cast<const VT*>(un_x + it_goff[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPS; ++k) {
+      sf_r[k] = sf_p[k] = sf_x[k] = T(0);
+      if constexpr (VEC) {
+        const int m = is_meta[k];
+        if (last || !(m & (1 << 21))) continue;
+        sf_r[k] = un_r[is_goff[k]];
+        if constexpr (MODE == kFusedCG) {
+          sf_p[k] = un_p[is_goff[k]];
+          if (xupd && (m & (1 << 23))) sf_x[k] = un_x[is_goff[k]];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < (VEC ? 0 : NPF); ++k) {
       pf_r[k] = T(0);
       pf_p[k] = T(0);
       pf_x[k] = T(0);
@@ -1002,6 +1084,90 @@ BDX_PRAGMA_UNROLL(2)
       }
 
     };
+    auto do_stage_vec = [&]() __attribute__((always_inline)) {
+      // ------------------------------------------------ stage the next layer (VEC items)
+      if (!last) {
+#pragma unroll
+        for (int k = 0; k < NPI; ++k)
+          asm volatile("" : "+v"(it_goff[k]), "+v"(it_meta[k]), "+v"(it_lds[k]));
+#pragma unroll
+        for (int k = 0; k < NPS; ++k)
+          asm volatile("" : "+v"(is_goff[k]), "+v"(is_meta[k]), "+v"(is_lds[k]));
+        T* __restrict__ un = s_u[nxt];
+#pragma unroll
+        for (int k = 0; k < NCP; ++k)
+          if (cp_lds[k] >= 0) un[cp_lds[k]] = su[P * PLP + cp_lds[k]];
+        T* __restrict__ pnl = A.pnew + lnext;
+        T* __restrict__ yl = A.y + lnext;
+        // node e of an item: Dirichlet identity row (plane 0 of the march is
+        // the prologue's); returns the value staged into LDS
+        auto dirichlet = [&](int m, int e, unsigned goff, T v) __attribute__((always_inline)) -> T {
+          const int f = (m >> (4 * e)) & 15;
+          const int gxx = (cx + 1) * P + ((m >> 16) & 15);
+          if (!(f & kValid)) return T(0);
+          if ((f & kBcYZ) || gxx == A.bcx_hi) {
+            if (f & kOwnT) {
+              const bool rown = (f & kRownYZ) && gxx < A.ownx;
+              yl[goff + e] = rown ? v : T(0);
+              if constexpr (MODE == kFusedCG) {
+                if (rown) pap += static_cast<double>(v) * static_cast<double>(v);
+              }
+            }
+            return T(0);
+          }
+          return v;
+        };
+#pragma unroll
+        for (int k = 0; k < NPI; ++k) {
+          const int m = it_meta[k];
+          VT val;
+          if constexpr (MODE == kFusedCG) {
+            val = vf_r[k] + beta * vf_p[k];
+            const VT xn = vf_x[k] + xalpha * vf_p[k];
+            if (m & (1 << 22)) {  // every node owned: whole vectors
+              *reinterpret_cast<VT*>(pnl + it_goff[k]) = val;
+              if (xupd) *reinterpret_cast<VT*>(un_x + it_goff[k]) = xn;
+            } else if (m & (1 << 23)) {  // some owned (a tile at the domain's edge)
+#pragma unroll
+              for (int e = 0; e < V; ++e) {
+                if (!((m >> (4 * e)) & kOwnT)) continue;
+                pnl[it_goff[k] + e] = val[e];
+                if (xupd) un_x[it_goff[k] + e] = xn[e];
+              }
+            }
+          } else {
+            val = vf_r[k];
+          }
+#pragma unroll
+          for (int e = 0; e < V; ++e) un[it_lds[k] + e] = dirichlet(m, e, it_goff[k], val[e]);
+        }
+#pragma unroll
+        for (int k = 0; k < NPS; ++k) {
+          const int m = is_meta[k];
+          T val;
+          if constexpr (MODE == kFusedCG) {
+            val = sf_r[k] + beta * sf_p[k];
+            if (m & (1 << 23)) {
+              pnl[is_goff[k]] = val;
+              if (xupd) un_x[is_goff[k]] = sf_x[k] + xalpha * sf_p[k];
+            }
+          } else {
+            val = sf_r[k];
+          }
+          if (tid + k * NT < NITS) un[is_lds[k]] = dirichlet(m, 0, is_goff[k], val);
+        }
+#pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][e] = sX[NV + e];
+        }
+#pragma unroll
+        for (int k = 0; k < NPV; ++k) {
+          const int e = tid + k * NT;
+          if (e < NV) s_X[nxt][NV + e] = pf_v[k];
+        }
+      }
+    };
     auto do_stage = [&]() __attribute__((always_inline)) {
       // ------------------------------------------------ stage the next layer
       if (!last) {
@@ -1062,7 +1228,10 @@ BDX_PRAGMA_UNROLL(2)
     // Consume the prefetch before the gather stores,
     // behind one explicit vmcnt(0) (as in lap_fused5.h)
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    do_stage();
+    if constexpr (VEC)
+      do_stage_vec();
+    else
+      do_stage();
     do_gather();
     kc_cur = kc_nxt;
   }
@@ -1076,12 +1245,38 @@ BDX_PRAGMA_UNROLL(2)
 // Host-side launch: build the argument block from the packed lattice
 // descriptor (fem/mesh.py LocalLattice.as_int64) and launch one workgroup per
 // (y, z) tile.
+// Does a tile row's own part split into whole 16-byte vectors (the VEC
+// instance)?  Shape (compile time) and layout / alignment (launch time).
+template <typename T, int ND, int NQ>
+constexpr bool f3_vec_shape() {
+  constexpr int V = 16 / static_cast<int>(sizeof(T)), OWNZ = TileFor<NQ>::TZ * (ND - 1);
+  return kF3Vec && OWNZ % V == 0 && (OWNZ * static_cast<int>(sizeof(T))) % 16 == 0;
+}
+template <typename T, int ND, int NQ>
+bool f3_vec_ok(const Fused2Args<T>& a) {
+  constexpr int V = 16 / static_cast<int>(sizeof(T)), P = ND - 1;
+  constexpr int OWNY = TileFor<NQ>::TY * P, OWNZ = TileFor<NQ>::TZ * P;
+  const bool lay = a.tsy ? (a.tsy == OWNY && a.tsz == OWNZ)
+                         : (a.ld % V == 0 && a.ps % V == 0 && static_cast<int64_t>(a.ntz) * OWNZ <= a.ld);
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return lay && al(a.u) && al(a.pold) && al(a.pnew) && al(a.x);
+}
+
 template <typename T, int ND, int NQ, int MODE>
 int launch_fused3(int affine, const Fused2Args<T>& a, const FusedTables<T>& tb, hipStream_t st) {
   using TF = TileFor<NQ>;
   using S = FusedShape<T, ND, NQ, TF::TY, TF::TZ>;
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
+  if constexpr (MODE == kFusedCG && f3_vec_shape<T, ND, NQ>()) {
+    if (affine != 1 && f3_vec_ok<T, ND, NQ>(a)) {
+      if (affine == 2)
+        lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 2, true><<<nblk, S::threads, 0, st>>>(a, tb);
+      else
+        lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 0, true><<<nblk, S::threads, 0, st>>>(a, tb);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   // affine: 1 = parallelepipeds, 2 = x-trilinear (y/z lattice), 0 = trilinear
   if (affine == 1)
     lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, MODE, 1><<<nblk, S::threads, 0, st>>>(a, tb);
@@ -1105,9 +1300,11 @@ int fused3_resident(int affine) {
       affine == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                         &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 1>, S::threads, 0)
       : affine == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                          &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 2>, S::threads, 0)
+                          &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 2,
+                                                     f3_vec_shape<T, ND, NQ>()>, S::threads, 0)
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                          &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 0>, S::threads, 0);
+                          &per_cu, lap_fused3_kernel<T, ND, NQ, TF::TY, TF::TZ, kFusedCG, 0,
+                                                     f3_vec_shape<T, ND, NQ>()>, S::threads, 0);
   return e == hipSuccess ? per_cu * cus : 0;
 }
 
