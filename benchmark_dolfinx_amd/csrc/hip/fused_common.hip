@@ -30,6 +30,7 @@ int pack_tables(const double* phi0, const double* dphi1, T* out) {
 // slots of the partials buffer, then one block): deterministic like the rest.
 constexpr int kPartialsCap = 65536, kStage1 = 256;
 constexpr int kUpdGrid = kPartialsCap - kStage1;  // update pass grid cap
+constexpr int kUpdU = 2;  // vectors per thread of the tiled update pass
 
 // CG update of the fused2..5 paths: alpha = s[rn] / s[pap];
 //   r -= alpha (y + interface partials);  partial r.r
@@ -121,7 +122,12 @@ __global__ void __launch_bounds__(256)
 // update 1.555 -> 1.583 ms), same box (scripts/r3_updrow.sh).  Blocks stay in
 // launch order: an XCD-aware remap (contiguous slabs per XCD) made the pass
 // 8-40 % slower (Q6 FP64 update 2.54 -> 3.54 ms, scripts/r3_updxcd.sh).
-template <typename T, bool ROW>
+// Round 4: U = 2 vectors per thread with both loads in flight, and the chunk ->
+// (tile, x) split in 32-bit arithmetic (it was two 64-bit divisions per
+// vector): update pass Q3 1.79 -> 1.54 ms, Q6 2.76 -> 2.59, Q6 FP32 1.58 ->
+// 1.37, same box (U = 1: 1.57 at Q3, U = 4: no gain;
+// profiles/r4_update_pass_ab.txt).
+template <typename T, bool ROW, int U>
 __global__ void __launch_bounds__(256)
     cg_update_tiled_kernel(int64_t L0, int64_t L1, int64_t Lz, int tsy, int tsz, int tntz,
                            int64_t o0, int64_t o1, int64_t o2, int64_t nvec, T* __restrict__ r,
@@ -134,81 +140,104 @@ __global__ void __launch_bounds__(256)
   constexpr int W = 16 / sizeof(T);
   typedef T V __attribute__((ext_vector_type(W)));
   const int64_t ch = static_cast<int64_t>(tsy) * tsz;
-  const double inv_ch = 1.0 / static_cast<double>(ch), inv_l0 = 1.0 / static_cast<double>(L0);
+  const double inv_ch = 1.0 / static_cast<double>(ch);
+  const float inv_l0 = 1.0f / static_cast<float>(L0), inv_tntz = 1.0f / static_cast<float>(tntz);
   const float inv_tsz = 1.0f / static_cast<float>(tsz);
+  const int l0 = static_cast<int>(L0);
   double acc = 0.0;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * 256) {
-    const int64_t e0 = v * W;
-    int64_t c = static_cast<int64_t>(static_cast<double>(e0) * inv_ch);  // chunk
-    if (c * ch > e0) --c;
-    if ((c + 1) * ch <= e0) ++c;
-    int64_t blk = static_cast<int64_t>(static_cast<double>(c) * inv_l0);
-    if (blk * L0 > c) --blk;
-    if ((blk + 1) * L0 <= c) ++blk;
-    const int64_t x = c - blk * L0;
-    const int tY = static_cast<int>(blk / tntz), tZ = static_cast<int>(blk - static_cast<int64_t>(tY) * tntz);
-    if (x >= o0) continue;
-    const int ein = static_cast<int>(e0 - c * ch);
-    if (BDX_OOB(e0 + W - 1, nvec * W, "tiled update")) continue;
-    // (y, z) of the vector's first element
-    int ly = static_cast<int>(static_cast<float>(ein) * inv_tsz);
-    if (ly * tsz > ein) --ly;
-    if ((ly + 1) * tsz <= ein) ++ly;
-    if constexpr (ROW) {
-      const int lz0 = ein - ly * tsz;
-      const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz0 = static_cast<int64_t>(tZ) * tsz + lz0;
-      if (gy >= o1 || gz0 >= o2) continue;
-      V t = *reinterpret_cast<const V*>(y + e0);
-      V vr = *reinterpret_cast<const V*>(r + e0);
-      const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
-      const int nw = o2 - gz0 < W ? static_cast<int>(o2 - gz0) : W;  // owned elements
-      if (yrow >= 0) {
-        const T* yr = yb + (x * (nty - 1) + yrow) * Lz + gz0;
+  for (int64_t vb = static_cast<int64_t>(blockIdx.x) * (256 * U) + threadIdx.x; vb < nvec;
+       vb += static_cast<int64_t>(gridDim.x) * (256 * U)) {
+    // U vectors per thread, 256 apart (each load coalesced over the block), all
+    // loads in flight before the index math and the arithmetic
+    V vyu[U], vru[U];
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (w < nw) t[w] += yr[w];
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = vb + u * 256;
+      if (v < nvec) {
+        vyu[u] = *reinterpret_cast<const V*>(y + v * W);
+        vru[u] = *reinterpret_cast<const V*>(r + v * W);
       }
-      if (lz0 == 0 && tZ >= 1 && tZ < ntz) {
-        t[0] += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
-        if (yrow >= 0) t[0] += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
-      }
+    }
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const T rn = vr[w] - alpha * t[w];
-        if (w < nw) {
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = vb + u * 256;
+      if (v >= nvec) break;
+      const int64_t e0 = v * W;
+      int64_t c = static_cast<int64_t>(static_cast<double>(e0) * inv_ch);  // chunk
+      if (c * ch > e0) --c;
+      if ((c + 1) * ch <= e0) ++c;
+      // chunk -> (tile, x): 32-bit (chunks < 2^31), float reciprocals + exact fix-ups
+      const int ci = static_cast<int>(c);
+      int blk = static_cast<int>(static_cast<float>(ci) * inv_l0);
+      while (blk * l0 > ci) --blk;
+      while ((blk + 1) * l0 <= ci) ++blk;
+      const int x = ci - blk * l0;
+      int tY = static_cast<int>(static_cast<float>(blk) * inv_tntz);
+      while (tY * tntz > blk) --tY;
+      while ((tY + 1) * tntz <= blk) ++tY;
+      const int tZ = blk - tY * tntz;
+      if (x >= o0) continue;
+      const int ein = static_cast<int>(e0 - c * ch);
+      if (BDX_OOB(e0 + W - 1, nvec * W, "tiled update")) continue;
+      // (y, z) of the vector's first element
+      int ly = static_cast<int>(static_cast<float>(ein) * inv_tsz);
+      if (ly * tsz > ein) --ly;
+      if ((ly + 1) * tsz <= ein) ++ly;
+      if constexpr (ROW) {
+        const int lz0 = ein - ly * tsz;
+        const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz0 = static_cast<int64_t>(tZ) * tsz + lz0;
+        if (gy >= o1 || gz0 >= o2) continue;
+        V t = vyu[u];
+        V vr = vru[u];
+        const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
+        const int nw = o2 - gz0 < W ? static_cast<int>(o2 - gz0) : W;  // owned elements
+        if (yrow >= 0) {
+          const T* yr = yb + (x * (nty - 1) + yrow) * Lz + gz0;
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if (w < nw) t[w] += yr[w];
+        }
+        if (lz0 == 0 && tZ >= 1 && tZ < ntz) {
+          t[0] += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
+          if (yrow >= 0) t[0] += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const T rn = vr[w] - alpha * t[w];
+          if (w < nw) {
+            vr[w] = rn;
+            acc += static_cast<double>(rn) * static_cast<double>(rn);
+          }
+        }
+        *reinterpret_cast<V*>(r + e0) = vr;
+      } else {
+        const V vy = vyu[u];
+        V vr = vru[u];
+        bool any = false;
+        // the other elements step along z
+        int lz = ein - ly * tsz - 1;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          if (++lz == tsz) {
+            lz = 0;
+            ++ly;
+          }
+          const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz = static_cast<int64_t>(tZ) * tsz + lz;
+          if (gy >= o1 || gz >= o2) continue;
+          any = true;
+          const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
+          T t = vy[w];
+          if (yrow >= 0) t += yb[(x * (nty - 1) + yrow) * Lz + gz];
+          if (lz == 0 && tZ >= 1 && tZ < ntz) {
+            t += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
+            if (yrow >= 0) t += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
+          }
+          const T rn = vr[w] - alpha * t;
           vr[w] = rn;
           acc += static_cast<double>(rn) * static_cast<double>(rn);
         }
+        if (any) *reinterpret_cast<V*>(r + e0) = vr;
       }
-      *reinterpret_cast<V*>(r + e0) = vr;
-    } else {
-      const V vy = *reinterpret_cast<const V*>(y + e0);
-      V vr = *reinterpret_cast<const V*>(r + e0);
-      bool any = false;
-      // the other elements step along z
-      int lz = ein - ly * tsz - 1;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        if (++lz == tsz) {
-          lz = 0;
-          ++ly;
-        }
-        const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz = static_cast<int64_t>(tZ) * tsz + lz;
-        if (gy >= o1 || gz >= o2) continue;
-        any = true;
-        const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
-        T t = vy[w];
-        if (yrow >= 0) t += yb[(x * (nty - 1) + yrow) * Lz + gz];
-        if (lz == 0 && tZ >= 1 && tZ < ntz) {
-          t += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
-          if (yrow >= 0) t += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
-        }
-        const T rn = vr[w] - alpha * t;
-        vr[w] = rn;
-        acc += static_cast<double>(rn) * static_cast<double>(rn);
-      }
-      if (any) *reinterpret_cast<V*>(r + e0) = vr;
     }
   }
   const double t = block_sum(acc, lds);
@@ -309,15 +338,15 @@ BDX_CGI(float, f32)
     if (!L.tsy || (L.tsy * L.tsz * static_cast<int64_t>(sizeof(T))) % 16)                     \
       return static_cast<int>(hipErrorInvalidValue);                                           \
     const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
-    const int64_t want = (nvec + 255) / 256;                                                   \
+    const int64_t want = (nvec + 256 * kUpdU - 1) / (256 * kUpdU);                             \
     const int g = static_cast<int>(want < kUpdGrid ? (want > 0 ? want : 1) : kUpdGrid); \
     if (sizeof(T) == 4 && L.tsz % 4 == 0)                                                      \
-      cg_update_tiled_kernel<T, true><<<g, 256, 0, st>>>(                                      \
+      cg_update_tiled_kernel<T, true, kUpdU><<<g, 256, 0, st>>>(                               \
           L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),            \
           static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,  \
           scal, rn_slot, pap_slot, partials);                                                  \
     else                                                                                       \
-      cg_update_tiled_kernel<T, false><<<g, 256, 0, st>>>(                                     \
+      cg_update_tiled_kernel<T, false, kUpdU><<<g, 256, 0, st>>>(                              \
           L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),            \
           static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,  \
           scal, rn_slot, pap_slot, partials);                                                  \
