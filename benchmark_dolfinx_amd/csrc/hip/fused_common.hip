@@ -126,7 +126,10 @@ __global__ void __launch_bounds__(256)
 // (tile, x) split in 32-bit arithmetic (it was two 64-bit divisions per
 // vector): update pass Q3 1.79 -> 1.54 ms, Q6 2.76 -> 2.59, Q6 FP32 1.58 ->
 // 1.37, same box (U = 1: 1.57 at Q3, U = 4: no gain;
-// profiles/r4_update_pass_ab.txt).
+// profiles/r4_update_pass_ab.txt).  The pass's r / y loads and r stores are
+// non-temporal (whole 16-byte vectors, full lines; unlike the operator's
+// march, nothing here relies on L2 merging partial rows): update Q3 1.53 ->
+// 1.46 ms, Q6 FP64 2.50 -> 2.30, +1.6-1.8 % GDoF/s same box (same file).
 template <typename T, bool ROW, int U>
 __global__ void __launch_bounds__(256)
     cg_update_tiled_kernel(int64_t L0, int64_t L1, int64_t Lz, int tsy, int tsz, int tntz,
@@ -154,8 +157,8 @@ __global__ void __launch_bounds__(256)
     for (int u = 0; u < U; ++u) {
       const int64_t v = vb + u * 256;
       if (v < nvec) {
-        vyu[u] = *reinterpret_cast<const V*>(y + v * W);
-        vru[u] = *reinterpret_cast<const V*>(r + v * W);
+        vyu[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(y + v * W));
+        vru[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(r + v * W));
       }
     }
 #pragma unroll
@@ -209,7 +212,7 @@ __global__ void __launch_bounds__(256)
             acc += static_cast<double>(rn) * static_cast<double>(rn);
           }
         }
-        *reinterpret_cast<V*>(r + e0) = vr;
+        __builtin_nontemporal_store(vr, reinterpret_cast<V*>(r + e0));
       } else {
         const V vy = vyu[u];
         V vr = vru[u];
@@ -236,7 +239,7 @@ __global__ void __launch_bounds__(256)
           vr[w] = rn;
           acc += static_cast<double>(rn) * static_cast<double>(rn);
         }
-        if (any) *reinterpret_cast<V*>(r + e0) = vr;
+        if (any) __builtin_nontemporal_store(vr, reinterpret_cast<V*>(r + e0));
       }
     }
   }
