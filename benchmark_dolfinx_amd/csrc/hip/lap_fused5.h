@@ -508,8 +508,12 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
         vf_r[k] = *reinterpret_cast<const VT*>(un_r + it_goff[k]);
         if constexpr (MODE == kFusedCG) {
           vf_p[k] = *reinterpret_cast<const VT*>(un_p + it_goff[k]);
-          if (xupd && (m & (1 << 23))) vf_x[k] = *reinterpret_cast<const VT*>(un_x + it_goff[k]);
-          if (xpair && (m & (1 << 23))) vf_q[k] = *reinterpret_cast<const VT*>(un_q + it_goff[k]);
+          // x and p_prev2 are read by this tile only (own nodes): streamed
+          // non-temporally, Q3 +2.1 % same box (profiles/r4_fused5_nt_ab.txt)
+          if (xupd && (m & (1 << 23)))
+            vf_x[k] = __builtin_nontemporal_load(reinterpret_cast<const VT*>(un_x + it_goff[k]));
+          if (xpair && (m & (1 << 23)))
+            vf_q[k] = __builtin_nontemporal_load(reinterpret_cast<const VT*>(un_q + it_goff[k]));
         }
       }
     }
@@ -804,8 +808,11 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
             VT xn = vf_x[k] + xalpha * vf_p[k];
             if (xpair) xn += xalpha2 * vf_q[k];
             if (m & (1 << 22)) {  // every node owned: whole vectors
-              *reinterpret_cast<VT*>(pnl + it_goff[k]) = val;
-              if (xupd) *reinterpret_cast<VT*>(un_x + it_goff[k]) = xn;
+              // non-temporal: whole 16-byte vectors of contiguous tile rows,
+              // not read again before the next iteration (Q3 +1.5 %, Q6 FP32
+              // +2.1 % same box, profiles/r4_fused5_nt_ab.txt)
+              __builtin_nontemporal_store(val, reinterpret_cast<VT*>(pnl + it_goff[k]));
+              if (xupd) __builtin_nontemporal_store(xn, reinterpret_cast<VT*>(un_x + it_goff[k]));
             } else if (m & (1 << 23)) {  // some owned (a tile at the domain's edge)
 #pragma unroll
               for (int e = 0; e < V; ++e) {
