@@ -71,6 +71,10 @@ constexpr int kScalXSave = 3;
 // 29.9, Q6 44.6 -> 28.9, Q6-FP32 59.3 -> 35.1 GDoF/s, profiles/r2_nt_ab.md):
 // the x-march writes 96-byte row segments, and only the default policy lets
 // L2 merge neighbouring tiles' segments into whole lines before write-back.
+// (Round 4: whole 16-byte-vector streams that no other tile re-reads -- the
+// update passes, fused5's own-node staging loads and stores -- do gain from
+// __builtin_nontemporal_*, see profiles/r4_fused5_nt_ab.txt; these helpers
+// keep the default policy for the element-wise accesses.)
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
   return *p;
