@@ -194,6 +194,8 @@ constexpr int kFeTiles = 16;  // tiles per flush_export block along z
 // vectors, stages the result in LDS in lattice order and writes the group's
 // z-rows contiguously, so both sides stream (the element-wise forms ran at
 // 2-3.7 TB/s: 64-bit divisions per element, then 96-byte lattice runs).
+// Every access is non-temporal (+0.2 % on the 20-step Q3 / Q6 runs that
+// carry one flush each, profiles/r4_update_pass_ab.txt).
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
     flush_export_kernel(int64_t L0, int64_t L1, int64_t L2, int64_t ld, int tsy, int tsz,
@@ -218,10 +220,10 @@ __global__ void __launch_bounds__(kBlock)
   for (int q = threadIdx.x; q < nt * CV; q += kBlock) {
     const int tl = q / CV, e = (q - tl * CV) * W;
     const int64_t off = (cbase + static_cast<int64_t>(tl) * L0) * C + e;
-    V vt = *reinterpret_cast<const V*>(t + off);
-    vt += a1 * *reinterpret_cast<const V*>(p1 + off);
-    if (p2) vt += a2 * *reinterpret_cast<const V*>(p2 + off);
-    *reinterpret_cast<V*>(t + off) = vt;
+    V vt = __builtin_nontemporal_load(reinterpret_cast<const V*>(t + off));
+    vt += a1 * __builtin_nontemporal_load(reinterpret_cast<const V*>(p1 + off));
+    if (p2) vt += a2 * __builtin_nontemporal_load(reinterpret_cast<const V*>(p2 + off));
+    __builtin_nontemporal_store(vt, reinterpret_cast<V*>(t + off));
     int ly = e / tsz, lz = e - ly * tsz;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -240,7 +242,7 @@ __global__ void __launch_bounds__(kBlock)
   const int nj = static_cast<int>((j0 + tsy <= L1) ? tsy : L1 - j0);
   for (int r = threadIdx.x; r < nj * nk; r += kBlock) {
     const int ly = r / nk, kk = r - ly * nk;
-    a[(x * L1 + j0 + ly) * ld + k0 + kk] = sv[ly * pitch + kk];
+    __builtin_nontemporal_store(sv[ly * pitch + kk], a + (x * L1 + j0 + ly) * ld + k0 + kk);
   }
 }
 
