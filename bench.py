@@ -293,7 +293,8 @@ def _measure_isolated(a, config, steps, warmup, *, kappa="constant", perturb=0.0
 class MeasurementFailed(RuntimeError):
     """A measurement failed on a multi-rank run: fatal (the other ranks may
     be inside a collective the failed rank will never join), but it carries
-    the records measured so far so rank 0 can still report them."""
+    the records measured so far (headline, companions, variants) so rank 0
+    can still report them."""
 
     def __init__(self, msg, partial):
         super().__init__(msg)
@@ -364,7 +365,7 @@ def run(comm, a) -> dict | None:
                     comm, a, c, a.steps, a.warmup, kappa=kap, perturb=a.perturb,
                     kernel=a.kernel, geometry=a.geometry, log=log), log)
             except Exception as e:
-                raise MeasurementFailed(f"{key}: {e!r}", (head, companions)) from e
+                raise MeasurementFailed(f"{key}: {e!r}", (head, companions, {})) from e
     extras = {}
     if gpu and (a.extras == "on" or (a.extras == "auto" and n == 1)):
         # north-star variants of the headline config (BASELINE.json: random
@@ -374,7 +375,7 @@ def run(comm, a) -> dict | None:
         # forces the fully general trilinear-geometry instance on the same
         # mesh; "dofmap" runs explicit cell->dof / cell->vertex arrays with G
         # stored per quadrature point, as the reference does.
-        vsteps = min(a.steps, 50)
+        # the headline's clock discipline: same --steps / --warmup
         pert = a.perturb or 0.1
         specs = (("general", a.config, dict(kappa=a.kappa, perturb=pert)),
                  ("general_trilinear", a.config, dict(kappa=a.kappa, perturb=pert,
@@ -396,12 +397,15 @@ def run(comm, a) -> dict | None:
                 continue
             kw.setdefault("kernel", a.kernel if kw.get("geometry") is None else "auto")
             kw.setdefault("geometry", a.geometry)
-            if isolate:
-                extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure_isolated(
-                    a, cfg, vsteps, 3, log=log, **kw), log)
-            else:
-                extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure(
-                    comm, a, cfg, vsteps, 3, log=log, **kw), log)
+            try:
+                if isolate:
+                    extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure_isolated(
+                        a, cfg, a.steps, a.warmup, log=log, **kw), log)
+                else:
+                    extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure(
+                        comm, a, cfg, a.steps, a.warmup, log=log, **kw), log)
+            except Exception as e:
+                raise MeasurementFailed(f"{key}: {e!r}", (head, companions, extras)) from e
     if comm.rank != 0:
         return None
     return _record(a, n, head, companions, extras, flags, gpu)
@@ -602,7 +606,7 @@ def main(argv=None) -> int:
             part = getattr(e, "partial", None)
             if part is not None:
                 try:
-                    rec.update(_record(a, comm.size, part[0], part[1], {}, None,
+                    rec.update(_record(a, comm.size, part[0], part[1], part[2], None,
                                        a.platform == "gpu"))
                     rec["error"] = repr(e)
                 except Exception:  # noqa: BLE001 - the error line must go out

@@ -9,7 +9,7 @@ Reference options (src/main.cpp:144-183): --platform, --float, --ndofs,
 --geom_perturb_fact, --use_gauss, --json.  Unknown options are accepted
 (like `allow_unregistered`, used for `SPDLOG_LEVEL=...`).
 
-MI355X extensions (additive): --kernel {auto,fused5,fused4,fused3,fused2,
+MI355X extensions (additive): --kernel {auto,fused5,fused3,fused2,
 fused,v1,dofmap}, --geometry {auto,otf,otf-general,stored}, --kappa {constant,random},
 --warmup N (untimed repetitions before the timed loop).
 The JSON gains an additive "mi355x" object; the reference keys are
@@ -56,7 +56,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--json", default="", help="Filename for JSON output")
     # MI355X extensions
     ap.add_argument("--kernel", default="auto",
-                    choices=["auto", "fused5", "fused4", "fused3", "fused2", "fused", "v1", "dofmap"],
+                    choices=["auto", "fused5", "fused3", "fused2", "fused", "v1", "dofmap"],
                     help="GPU operator kernel: fused structured kernel, the generic v1, or the "
                          "unstructured dofmap data model")
     ap.add_argument("--geometry", default="auto", choices=["auto", "otf", "otf-general", "stored"],

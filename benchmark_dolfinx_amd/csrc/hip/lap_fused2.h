@@ -63,7 +63,7 @@ struct Fused2Args {
   T kappa;
   // tiled vector storage (bdx_lattice.h; tsy = 0: lattice layout): the
   // x-plane stride ps is then tsy * tsz and a node's (y, z) offset is its
-  // tile's column base plus the in-tile position (fused4 / fused5 only)
+  // tile's column base plus the in-tile position (fused5 only)
   int tsy, tsz, tntz;
   int64_t tcol;
   int64_t vsize;   // elements of one vector (BDX_DEBUG bounds checks)

@@ -1,42 +1,46 @@
 // Fused structured operator kernel, v5 ("fused5"): nodal Kronecker sum
-// factorisation for parallelepiped cells, any degree P = 3..7, FP64 / FP32.
+// factorisation for axis-aligned box cells, any degree P = 3..7, FP64 / FP32.
 //
 // For a cell with a constant Jacobian the quadrature sum of the reference
 // stiffness operator (src/laplacian_gpu.hpp:91-426 with
 // src/geometry_gpu.hpp:26-132) factorises exactly into 1D matrices of the
-// same quadrature rule (see lap_fused4.h):
+// same quadrature rule:
 //   M = B^T W B,  K = Dd^T W Dd,  C = Dd^T W B   (B = phi0, Dd = dphi1 phi0),
 //   A_e = G00 K.M.M + G11 M.K.M + G22 M.M.K + G12 M.(C.Ct + Ct.C)
 //       + G01 (C.Ct.M + Ct.C.M) + G02 (C.M.Ct + Ct.M.C)      (x . y . z).
-// fused4 contracts the (y, z) factor as one 16 x 16 MFMA operand, which only
-// pays at ND = 4.  Here the three directions are applied one after another
+// On an axis-aligned box G01 = G02 = G12 = 0.  (An earlier core, fused4,
+// contracted the (y, z) factor as one 16 x 16 MFMA operand, which only paid
+// at ND = 4 and lost to this one; removed in round 5.)  Here the three
+// directions are applied one after another
 // on ND x ND nodal matrices -- no quadrature-point arrays at all (ND^3 instead
 // of NQ^3 values per cell, 343 vs 512 at Q6) -- with every pass reading its
 // input line once:
 //   x pass   lane (j, k) holds the x-line u[.][j][k] (slab LDS -> registers),
-//            forms Kx u, Mx u (+ Cx u, Ct_x u on sheared cells);
+//            forms Kx u, Mx u;
 //   z pass   lane (i, j) reads its z-lines (one 16-byte vector row each) and
 //            forms the y-factor groups
-//              zM  = G00 Mz(Kx u) + G22 Kz(Mx u) [+ G02 (Ctz(Cx u) + Cz(Ctx u))]
-//              zK  = G11 Mz(Mx u)
-//             [zCt = G01 Mz(Cx u) + G12 Cz(Mx u)]
-//             [zC  = G01 Mz(Ctx u) + G12 Ctz(Mx u)];
+//              zM  = G00 Mz(Kx u) + G22 Kz(Mx u)
+//              zK  = G11 Mz(Mx u);
 //   y pass   lane (i, k) reads its y-lines and forms
-//              y_e = My zM + Ky zK [+ Ct_y zCt + C_y zC].
+//              y_e = My zM + Ky zK.
 // A cell is one wave for ND >= 6 (ND^2 lanes of 64) and 2 / 4 cells share a
 // wave at ND = 5 / 4, so the passes exchange data only inside a wave:
 // wave-local syncs, in-place rewrites of one per-wave buffer, two workgroup
 // barriers per cell layer (gather and staging).  The 1D matrices are
 // wave-uniform scalar loads from a device buffer that each operator owns
 // (allocated at construction, passed by pointer: a captured hipGraph keeps
-// reading its own operator's tables).  On axis-aligned boxes
-// (diagonal Jacobians, the benchmark mesh; exact host check) the 2-array
-// instance runs: 7 ND^2 FMAs per lane and cell.
+// reading its own operator's tables).  The kernel runs on axis-aligned
+// boxes only (diagonal Jacobians, the benchmark mesh; exact host check):
+// two arrays of line rows, 7 ND^2 FMAs per lane and cell.  Parallelepipeds
+// with a full Jacobian (G01, G02, G12 != 0) take fused3's affine instance
+// (driver.py): the four-array form of this core for them was reachable only
+// from a test-only shear map and was removed in round 5.
 //
 // Everything around the core -- the x-march over (y, z) tiles, the double
 // buffered slab staging with the CG fusion (p = r + beta p_old, lagged
 // x update, Dirichlet identity rows, p.Ap partials as element dots) and the
-// atomic-free gather with tile-interface buffers -- is fused4's.
+// atomic-free gather with tile-interface buffers -- is shared with fused3's
+// x-march design (lap_fused2.h / lap_fused3.h).
 #pragma once
 #include <cmath>
 #include <cstdlib>
@@ -77,9 +81,7 @@ constexpr int kF5Tab = kF5EO + 2 * 32;
 //    gather's stores, behind one explicit vmcnt(0) (Q3 +4.1 %, Q6 +1.1 %).
 static_assert(kF5Tab <= kFusedTabMax, "fused5 tables exceed the kernarg table");
 
-// cells per wave and (y, z) tile per degree; NARR = 4 (sheared cells) keeps
-// the 2 x 2 tile at ND >= 6 (its per-wave buffers are twice as large).
-// Tile shapes: same-box A/Bs of 4x4 vs 4x2 at ND = 4 and 2x2 vs 2x1 at
+// cells per wave and (y, z) tile per degree.  Tile shapes: same-box A/Bs of 4x4 vs 4x2 at ND = 4 and 2x2 vs 2x1 at
 // ND = 7 kept these (profiles/r2_fused5_evenodd.md).
 template <int ND> struct F5Tile;
 template <> struct F5Tile<4> { static constexpr int CPW = 4, TY = 4, TZ = 4; };
@@ -88,7 +90,7 @@ template <> struct F5Tile<6> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 template <> struct F5Tile<7> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 template <> struct F5Tile<8> { static constexpr int CPW = 1, TY = 2, TZ = 2; };
 
-template <typename T, int ND, int NARR>
+template <typename T, int ND>
 struct F5Shape {
   static constexpr int P = ND - 1;
   static constexpr int CPW = F5Tile<ND>::CPW, TY = F5Tile<ND>::TY, TZ = F5Tile<ND>::TZ;
@@ -103,7 +105,7 @@ struct F5Shape {
   static constexpr int ARR = CPW * ND * ND * NDP;  // one array of line rows
   // element vectors for the gather: E[cell][j][k][i]
   static constexpr int RP = ND, P1 = ND * ND, PC = ND * ND * ND;
-  static constexpr int WB0 = NARR * ARR;
+  static constexpr int WB0 = 2 * ARR;  // arrays 0 (Kx u / zM) and 1 (Mx u / zK)
   static constexpr int WB = WB0 > CPW * PC ? WB0 : CPW * PC;  // per-wave buffer
   static constexpr int DY = TY * P + 1, DZ = TZ * P + 1, PL = DY * DZ;
   static constexpr int DZP = DZ | 1, PLP = DY * DZP;
@@ -112,7 +114,7 @@ struct F5Shape {
 // Does a tile row's own part split into whole 16-byte vectors (the VEC instance)?
 template <typename T, int ND>
 constexpr bool f5_vec_shape() {
-  using S = F5Shape<T, ND, 2>;
+  using S = F5Shape<T, ND>;
   constexpr int V = 16 / static_cast<int>(sizeof(T)), OWNZ = S::TZ * S::P;
   return kF5Vec && OWNZ % V == 0 && (OWNZ * static_cast<int>(sizeof(T))) % 16 == 0;
 }
@@ -120,15 +122,14 @@ constexpr bool f5_vec_shape() {
 // fused5: nodal x / z / y Kronecker passes for parallelepiped cells, P = 3..7.
 // (An MFMA form of the three passes lost to this VALU core at Q6 in both
 // precisions: profiles/r2_fused5_mfma.md, profiles/r3_mfma.md.)
-template <typename T, int ND, int NARR, int MODE, bool VEC = false>
-__global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
+template <typename T, int ND, int MODE, bool VEC = false>
+__global__ void __launch_bounds__((F5Shape<T, ND>::NT), kF5Waves)
     lap_fused5_kernel(Fused2Args<T> A, const T* __restrict__ tabd) {
-  using S = F5Shape<T, ND, NARR>;
+  using S = F5Shape<T, ND>;
   constexpr int P = S::P, CPW = S::CPW, TY = S::TY, TZ = S::TZ;
   constexpr int DY = S::DY, DZ = S::DZ, PL = S::PL, DZP = S::DZP, PLP = S::PLP;
   constexpr int NT = S::NT, ND2 = ND * ND, NDP = S::NDP, ARR = S::ARR, WB = S::WB;
   constexpr int RP = S::RP, P1 = S::P1, PC = S::PC;
-  constexpr bool MIXED = NARR == 4;
   // VEC: the next layer's loads and the staging's p / x stores move 16 bytes
   // per lane -- items of V consecutive z-nodes of a tile row (its OWNZ own
   // nodes) plus one single node (the z-neighbour's first column); the host
@@ -597,7 +598,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
 #pragma unroll
       for (int l = 0; l < ND; ++l) u[l] = ucell[l * PLP + la * DZP + lb];
       T o[ND];
-      // array 0: Kx u, array 1: Mx u [, 2: Cx u, 3: Ctx u]; rows [i][j][k]
+      // array 0: Kx u, array 1: Mx u; rows [i][j][k]
       auto put = [&](int arr) {
         T* w = Wc + arr * ARR + la * NDP + lb;
         if (lane_on) {
@@ -609,17 +610,11 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
       put(0);
       matvec(0, u, o, T(1), false);
       put(1);
-      if constexpr (MIXED) {
-        matvec(2, u, o, T(1), false);
-        put(2);
-        matvec(3, u, o, T(1), false);
-        put(3);
-      }
     }
     wave_sync();
 
     // ------------------------------------------------ z pass: lane (i, j) = (la, lb)
-    if constexpr (!MIXED) {
+    {
       // both input rows of every lane are in registers once the loads have
       // returned (one ds_read per row for the whole wave), so zK can be
       // written back before zM is formed: one output row live, not two
@@ -645,48 +640,6 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
         for (int k = 0; k < ND; ++k) w[k * NDP] = zM[k];
       }
       wave_sync();
-    } else {
-      const T* r = Wc + ab * NDP;
-      T ak[ND], am[ND];
-      ldrow<ND>(r, ak);
-      ldrow<ND>(r + ARR, am);
-      T zM[ND], zK[ND];
-      matvec(0, ak, zM, G00, false);
-      matvec(1, am, zM, G22, true);
-      matvec(0, am, zK, G11, false);
-      if constexpr (MIXED) {
-        T ac[ND], at[ND];
-        ldrow<ND>(r + 2 * ARR, ac);
-        ldrow<ND>(r + 3 * ARR, at);
-        T zCt[ND], zC[ND];
-        matvec(3, ac, zM, G02, true);
-        matvec(2, at, zM, G02, true);
-        matvec(0, ac, zCt, G01, false);
-        matvec(2, am, zCt, G12, true);
-        matvec(0, at, zC, G01, false);
-        matvec(3, am, zC, G12, true);
-        wave_sync();
-        // rows [i][k][j]: lane (i, j) writes column j of rows (i, k)
-        if (lane_on) {
-          T* w = Wc + la * ND * NDP + lb;
-#pragma unroll
-          for (int k = 0; k < ND; ++k) {
-            w[2 * ARR + k * NDP] = zCt[k];
-            w[3 * ARR + k * NDP] = zC[k];
-          }
-        }
-      } else {
-        wave_sync();
-      }
-      if (lane_on) {
-        T* w = Wc + la * ND * NDP + lb;
-#pragma unroll
-        for (int k = 0; k < ND; ++k) {
-          w[k * NDP] = zM[k];
-          w[ARR + k * NDP] = zK[k];
-        }
-      }
-      wave_sync();
     }
 
     // ------------------------------------------------ y pass: lane (i, k) = (la, lb)
@@ -698,13 +651,6 @@ __global__ void __launch_bounds__((F5Shape<T, ND, NARR>::NT), kF5Waves)
       ldrow<ND>(r + ARR, sK);
       matvec(0, sM, ye, T(1), false);
       matvec(1, sK, ye, T(1), true);
-      if constexpr (MIXED) {
-        T sCt[ND], sC[ND];
-        ldrow<ND>(r + 2 * ARR, sCt);
-        ldrow<ND>(r + 3 * ARR, sC);
-        matvec(3, sCt, ye, T(1), true);
-        matvec(2, sC, ye, T(1), true);
-      }
     }
     // element dot p_e . (A_e p_e): lane holds y_e[i = la][j][k = lb]
     if constexpr (MODE == kFusedCG) {
@@ -994,15 +940,15 @@ inline int pack_tables5(int nd, int nq, const double* phi0, const double* Dd, co
   return kFusedTabMax;
 }
 
-// affine_ok: 0 = general cells (refused), 1 = parallelepipeds, 2 = axis-aligned
-// boxes (diagonal Jacobians: the 2-array instance)
+// affine_ok: 2 = axis-aligned boxes (diagonal Jacobians); anything else is
+// refused (general parallelepipeds run fused3's affine instance)
 // Can the VEC instance run on this launch?  Every tile row's own nodes must
 // start on a 16-byte boundary: the tiled storage's tiles are the kernel's
 // (y, z) tiles, or the lattice rows are padded to whole vectors, and the
 // vectors themselves are 16-byte aligned.
 template <typename T, int ND>
 bool f5_vec_ok(const Fused2Args<T>& a) {
-  using S = F5Shape<T, ND, 2>;
+  using S = F5Shape<T, ND>;
   constexpr int V = 16 / static_cast<int>(sizeof(T)), OWNZ = S::TZ * S::P;
   if (OWNZ % V || (OWNZ * static_cast<int>(sizeof(T))) % 16) return false;
   // lattice layout: the padded row pitch holds every tile's vectors (the top
@@ -1015,18 +961,16 @@ bool f5_vec_ok(const Fused2Args<T>& a) {
 
 template <typename T, int ND, int MODE>
 int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStream_t st) {
+  if (affine_ok != 2) return static_cast<int>(hipErrorInvalidValue);
   const int nblk = a.nblk;
   if (nblk <= 0) return 0;
   if constexpr (MODE == kFusedCG && f5_vec_shape<T, ND>()) {
-    if (affine_ok == 2 && f5_vec_ok<T, ND>(a)) {
-      lap_fused5_kernel<T, ND, 2, MODE, true><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
+    if (f5_vec_ok<T, ND>(a)) {
+      lap_fused5_kernel<T, ND, MODE, true><<<nblk, F5Shape<T, ND>::NT, 0, st>>>(a, tabd);
       return static_cast<int>(hipGetLastError());
     }
   }
-  if (affine_ok == 2)
-    lap_fused5_kernel<T, ND, 2, MODE><<<nblk, F5Shape<T, ND, 2>::NT, 0, st>>>(a, tabd);
-  else
-    lap_fused5_kernel<T, ND, 4, MODE><<<nblk, F5Shape<T, ND, 4>::NT, 0, st>>>(a, tabd);
+  lap_fused5_kernel<T, ND, MODE><<<nblk, F5Shape<T, ND>::NT, 0, st>>>(a, tabd);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1078,15 +1022,11 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     hipError_t e = hipGetDevice(&dev);                                             \
     if (e == hipSuccess)                                                           \
       e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev); \
+    if (affine_ok != 2) return 1;                                                  \
     if (e == hipSuccess)                                                           \
-      e = affine_ok == 2                                                           \
-              ? hipOccupancyMaxActiveBlocksPerMultiprocessor(                      \
-                    &per_cu, lap_fused5_kernel<T, PP + 1, 2, kFusedCG,             \
-                                               f5_vec_shape<T, PP + 1>()>,             \
-                    F5Shape<T, PP + 1, 2>::NT, 0)                                  \
-              : hipOccupancyMaxActiveBlocksPerMultiprocessor(                      \
-                    &per_cu, lap_fused5_kernel<T, PP + 1, 4, kFusedCG>,            \
-                    F5Shape<T, PP + 1, 4>::NT, 0);                                 \
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(                            \
+          &per_cu, lap_fused5_kernel<T, PP + 1, kFusedCG, f5_vec_shape<T, PP + 1>()>, \
+          F5Shape<T, PP + 1>::NT, 0);                                              \
     return e == hipSuccess ? fused_choose_segments(tiles, ncx, per_cu * cus) : 1;  \
   }                                                                                \
   extern "C" int bdx_fused5_tile_p##PP##_##SUF(int affine_ok, int* ty, int* tz) {  \

@@ -93,7 +93,7 @@ int bdx_cg_update_tiled_f32(const int64_t*, const int64_t*, float*, const float*
                             hipStream_t);
 }
 
-// The fused2..5 operator entry points (lap_fused{2,3,4,5}_<suf>_p<P>.hip);
+// The fused2, fused3 and fused5 operator entry points (lap_fused{2,3,5}_<suf>_p<P>.hip);
 // weak so that experiment builds holding a subset of the operator TUs still
 // load (a missing instance resolves to null and bdx_rt_create refuses it).
 #define BDX_DECL_APPLY(V, T, SUF, PP)                                                        \
@@ -111,7 +111,6 @@ int bdx_cg_update_tiled_f32(const int64_t*, const int64_t*, float*, const float*
   BDX_DECL_APPLY(V, float, f32, 6) BDX_DECL_APPLY(V, float, f32, 7)
 BDX_DECL_ALL(2)
 BDX_DECL_ALL(3)
-BDX_DECL_APPLY(4, double, f64, 3)
 #define BDX_DECL_F5(T, SUF) \
   BDX_DECL_APPLY(5, T, SUF, 3) BDX_DECL_APPLY(5, T, SUF, 4) BDX_DECL_APPLY(5, T, SUF, 5) \
   BDX_DECL_APPLY(5, T, SUF, 6) BDX_DECL_APPLY(5, T, SUF, 7)
@@ -151,8 +150,8 @@ ApplyFn<double> apply_fn<double>(int version, int P) {
   if (version == V && P == PP) return bdx_fused##V##_apply_f64_p##PP;
   BDX_CASE(2, 1) BDX_CASE(2, 2) BDX_CASE(2, 3) BDX_CASE(2, 4) BDX_CASE(2, 5) BDX_CASE(2, 6)
   BDX_CASE(2, 7) BDX_CASE(3, 1) BDX_CASE(3, 2) BDX_CASE(3, 3) BDX_CASE(3, 4) BDX_CASE(3, 5)
-  BDX_CASE(3, 6) BDX_CASE(3, 7) BDX_CASE(4, 3) BDX_CASE(5, 3) BDX_CASE(5, 4) BDX_CASE(5, 5)
-  BDX_CASE(5, 6) BDX_CASE(5, 7)
+  BDX_CASE(3, 6) BDX_CASE(3, 7) BDX_CASE(5, 3) BDX_CASE(5, 4) BDX_CASE(5, 5) BDX_CASE(5, 6)
+  BDX_CASE(5, 7)
 #undef BDX_CASE
   return nullptr;
 }
@@ -804,7 +803,7 @@ struct CGRuntime final : LoopBase {
   RtConfig cfg;
   ApplyFn<T> apply = nullptr;
   std::vector<T> tabs_host;
-  const T* tabs = nullptr;  // host copy (fused2-4: kernarg tables) or device buffer (fused5)
+  const T* tabs = nullptr;  // host copy (fused2/3: kernarg tables) or device buffer (fused5)
   T *x, *r, *pa, *pb, *y, *yb, *zb, *cb;
   // Tiled storage (cfg.latdT[17] != 0): the iteration runs on tiled copies
   // xt, rt, pat, pbt, yt (allocated zeroed by the caller: the padding stays
@@ -1232,7 +1231,7 @@ LoopBase* create(const int64_t* latd, const int64_t* own, const int* iparams, do
   rt->is_tiled = c.latdT[17] != 0;
   if (rt->is_tiled) {
     // only the x-march kernels whose tile is the storage tile address it
-    if ((c.version < 3 || c.version > 5) || c.latdT[17] != c.sy || c.latdT[18] != c.sz)
+    if ((c.version != 3 && c.version != 5) || c.latdT[17] != c.sy || c.latdT[18] != c.sz)
       return nullptr;
     rt->xt = static_cast<T*>(tptrs[0]);
     rt->rt_ = static_cast<T*>(tptrs[1]);

@@ -98,8 +98,10 @@ class Watchdog {
   bool fired() const { return fired_.load(); }
   int reason() const { return reason_.load(); }  // 0 none, 1 deadline, 2 async error
   double timeout_s() const { return timeout_ns_.load() * 1e-9; }
-  // A shorter (or longer) deadline for the scopes opened from now on (the
-  // bench pre-flight bounds its first exchange far below the run deadline).
+  // A shorter (or longer) deadline (the bench pre-flight bounds its first
+  // exchange far below the run deadline).  check() reads the deadline on
+  // every poll, so it applies at once to every open Busy scope, including
+  // one already open on another thread -- not only to scopes opened later.
   void set_timeout(double timeout_s) { timeout_ns_.store(static_cast<int64_t>(timeout_s * 1e9)); }
 
  private:

@@ -50,18 +50,15 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
             # (profiles/r2_xtrilinear.md: Q3 26.2, Q6 29.1 GDoF/s)
             kernel = "fused3"
         else:
-            # Kronecker cores on parallelepiped meshes.  fused5 (nodal sum
-            # factorisation) on axis-aligned boxes at every P >= 3: since the
-            # descriptor laundering (profiles/r2_launder.md) it beats the
-            # fused4 MFMA core at Q3 FP64 (58.4 vs 52.1 GDoF/s, same box,
-            # scripts/job_r2ac.sh).  Sheared parallelepipeds keep fused4 at
-            # Q3 (fused5's 4-array instance halves its occupancy there).
+            # fused5 (nodal Kronecker sum factorisation) on axis-aligned boxes
+            # at every P >= 3 (the benchmark mesh); parallelepipeds with a full
+            # Jacobian take fused3's affine instance.  The fused4 MFMA
+            # Kronecker core (beaten by fused5 at Q3 FP64 since
+            # profiles/r2_launder.md: 58.4 vs 52.1 GDoF/s) and fused5's
+            # sheared-cell instance were reachable only from a test-only
+            # shear map and were removed in round 5.
             from .models.fused import fused_supported
-            f5 = fused_supported(pb, 5)
-            if f5 and pb.all_axis_aligned:
-                auto = "fused5"
-            else:
-                auto = ("fused4" if fused_supported(pb, 4) else "fused5" if f5 else "fused3")
+            auto = "fused5" if fused_supported(pb, 5) else "fused3"
             kernel = os.environ.get("BDX_AUTO_AFFINE", auto)
     if kernel == "dofmap":
         # the unstructured data model: explicit cell->dof / cell->vertex maps
@@ -71,11 +68,6 @@ def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "aut
         from .models.fused import FusedLaplacianGPU, fused_supported
         if fused_supported(pb, 5) and geometry in ("auto", "otf"):
             return FusedLaplacianGPU(pb, geometry="otf", version=5)
-        kernel = "fused3"
-    if kernel == "fused4":
-        from .models.fused import FusedLaplacianGPU, fused_supported
-        if fused_supported(pb, 4) and geometry in ("auto", "otf"):
-            return FusedLaplacianGPU(pb, geometry="otf", version=4)
         kernel = "fused3"
     if kernel == "fused3":
         from .models.fused import FusedLaplacianGPU, fused_supported

@@ -34,8 +34,8 @@ def fused_supported(pb, version: int = 1) -> bool:
     lib = native.hip()
     if version == 3 and pb.tables.is_identity:
         return False  # fused3 is the phi0 != I core
-    if version in (4, 5) and not pb.all_affine:
-        return False  # the Kronecker cores need a constant Jacobian per cell
+    if version == 5 and not pb.all_axis_aligned:
+        return False  # the Kronecker core needs a diagonal Jacobian per cell
     v = "" if version == 1 else str(version)
     return hasattr(lib, f"bdx_fused{v}_apply_{pb.suf}_p{pb.degree}")
 
@@ -43,10 +43,9 @@ def fused_supported(pb, version: int = 1) -> bool:
 class FusedLaplacianGPU:
     """version=1: lap_fused.h (OTF or stored G); version=2: lap_fused2.h
     (OTF only, precomputed per-thread addressing); version=3: lap_fused3.h
-    (fused2 + direct-gradient contraction core, phi0 != I only); version=4:
-    lap_fused4.h (MFMA Kronecker core for parallelepiped cells, FP64 Q3);
-    version=5: lap_fused5.h (nodal Kronecker sum factorisation for
-    parallelepiped cells, P = 3..7, FP64 / FP32)."""
+    (fused2 + direct-gradient contraction core, phi0 != I only); version=5:
+    lap_fused5.h (nodal Kronecker sum factorisation for axis-aligned box
+    cells, P = 3..7, FP64 / FP32)."""
 
     def __init__(self, pb, geometry: str = "otf", version: int = 1, affine: bool = True,
                  runtime: str = "native", xtri: bool | None = None):
@@ -64,12 +63,12 @@ class FusedLaplacianGPU:
         # fused2: constant-Jacobian kernel instance when every local cell is a
         # parallelepiped (bitwise edge check on the host); else the trilinear one
         self.affine = bool(affine and pb.all_affine)
-        if version in (4, 5) and not self.affine:
-            raise ValueError(f"fused{version} needs parallelepiped cells (constant Jacobian)")
-        # kernel-instance selector passed as `affine_ok`: fused5 takes 2 on
-        # axis-aligned boxes (diagonal Jacobians: the 2-array instance)
+        if version == 5 and not (self.affine and pb.all_axis_aligned):
+            raise ValueError("fused5 needs axis-aligned box cells (diagonal Jacobian)")
+        # kernel-instance selector passed as `affine_ok`: fused5 runs on
+        # axis-aligned boxes only (2: diagonal Jacobians)
         self.affine_code = int(self.affine)
-        if version == 5 and pb.all_axis_aligned:
+        if version == 5:
             self.affine_code = 2
         # fused2/3 take 2 on x-trilinear meshes (y/z on the lattice, the
         # reference's --geom_perturb_fact class): the 16-operation per-point
@@ -90,9 +89,7 @@ class FusedLaplacianGPU:
         t = pb.kernels.t
         self.t = t
         ty, tz = ctypes.c_int(0), ctypes.c_int(0)
-        if version == 4:
-            _check(self.lib.bdx_fused4_tile(ctypes.byref(ty), ctypes.byref(tz)), "fused4_tile")
-        elif version == 5:
+        if version == 5:
             _check(getattr(self.lib, f"bdx_fused5_tile_p{pb.degree}_{pb.suf}")(
                 self.affine_code, ctypes.byref(ty), ctypes.byref(tz)), "fused5_tile")
         else:
@@ -115,7 +112,6 @@ class FusedLaplacianGPU:
         self.nseg = 1
         seg_fn = {2: f"bdx_fused2_segments_{pb.suf}_p{pb.degree}",
                   3: f"bdx_fused3_segments_{pb.suf}_p{pb.degree}",
-                  4: "bdx_fused4_segments",
                   5: f"bdx_fused5_segments_{pb.suf}_p{pb.degree}"}.get(version)
         if seg_fn and hasattr(self.lib, seg_fn):
             forced = os.environ.get("BDX_SEGMENTS", "")
@@ -146,16 +142,6 @@ class FusedLaplacianGPU:
                 raise RuntimeError(f"no fused5 tables for nd={t.nd} nq={t.nq}")
             host = np.zeros(ntab, dtype=np.float64 if pb.dtype == torch.float64 else np.float32)
             ftab5(t.nd, t.nq, ptr(t.phi0), ptr(self._Dd), ptr(wts), ptr(host))
-        elif version == 4:
-            # 1D mass / stiffness / mixed matrices of the quadrature rule
-            self._Dd = np.ascontiguousarray(pb.tables.Dd, dtype=np.float64)
-            ftab4 = getattr(self.lib, f"bdx_fused4_tables_{pb.suf}")
-            wts = np.ascontiguousarray(t.wts, dtype=np.float64)
-            ntab = ftab4(t.nd, t.nq, ptr(t.phi0), ptr(self._Dd), ptr(wts), None)
-            if ntab <= 0:
-                raise RuntimeError(f"no fused4 tables for nd={t.nd} nq={t.nq}")
-            host = np.zeros(ntab, dtype=np.float64)
-            ftab4(t.nd, t.nq, ptr(t.phi0), ptr(self._Dd), ptr(wts), ptr(host))
         else:
             if version == 3:
                 self._Dd = np.ascontiguousarray(pb.tables.Dd, dtype=np.float64)

@@ -166,6 +166,11 @@ class DofmapLaplacianGPU:
         self._cg = None
         self._rt = None
         import os
+        # native (default) at every rank count.  Its multi-rank split schedule
+        # is verified with thread ranks on one GPU (tests/test_gpu_dofmap.py)
+        # and shares the RCCL transport of the fused runtime; a run of it on
+        # separate GPUs has not been recorded yet (docs/PARITY.md).
+        # BDX_DOFMAP_RUNTIME=python selects the Python driver.
         self.runtime = runtime or os.environ.get("BDX_DOFMAP_RUNTIME", "native")
 
     def close(self) -> None:
@@ -228,7 +233,10 @@ class DofmapLaplacianGPU:
 
     def cg_iterate(self, cg, n: int, flush: bool = True) -> None:
         """n fused CG iterations; `flush=False` leaves the last lagged x
-        update pending (a later call or `flush` applies it)."""
+        update pending (a later call or `flush` applies it).  The native
+        runtime ignores `flush` (as the fused operators' does): its
+        iterate() always folds the pending x term at the end of the call,
+        so x is current after every call."""
         if self._rt is not None:
             return self._rt.iterate(n)
         pb, k = self.pb, self.k

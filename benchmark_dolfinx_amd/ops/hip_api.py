@@ -59,19 +59,12 @@ def declare(lib) -> None:
         _d(lib, f"bdx_xflush_{suf}", [vp, vp, vp, vp, vp, i32, i32, vp])
         _d(lib, f"bdx_fused_tables_{suf}", [i32, i32, vp, vp, vp])
         _d(lib, f"bdx_fused3_tables_{suf}", [i32, i32, vp, vp, vp])
-        if hasattr(lib, f"bdx_fused4_tables_{suf}"):
-            _d(lib, f"bdx_fused4_tables_{suf}", [i32, i32, vp, vp, vp, vp])
         for P in range(1, 8):
             if hasattr(lib, f"bdx_fused5_tables_{suf}_p{P}"):
                 _d(lib, f"bdx_fused5_tables_{suf}_p{P}", [i32, i32, vp, vp, vp, vp])
                 _d(lib, f"bdx_fused5_tile_p{P}_{suf}", [i32, vp, vp])
                 _d(lib, f"bdx_fused5_segments_{suf}_p{P}", [i32, i32, i32])
     _d(lib, "bdx_fused_tile", [i32, vp, vp])
-    if hasattr(lib, "bdx_fused4_tile"):
-        _d(lib, "bdx_fused4_tile", [vp, vp])
-    for name in ("bdx_fused4_segments",):
-        if hasattr(lib, name):
-            _d(lib, name, [i32, i32])
     # native CG runtime (runtime.hip)
     _d(lib, "bdx_rt_nccl_unique_id", [vp])
     _d(lib, "bdx_rt_rccl_selftest", [vp, i32, vp])

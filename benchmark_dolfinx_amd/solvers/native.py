@@ -135,7 +135,7 @@ class NativeCGRuntime:
         # Tiled vector storage for the x-march kernels: each (y, z) tile's
         # patch of an x-plane is contiguous, so the kernels' writes are whole
         # lines (profiles/r2_march_bw.md).  BDX_TILED=0: the lattice layout;
-        # 1 (default): fused4 / fused5 and fused3's x-trilinear instance
+        # 1 (default): fused5 and fused3's x-trilinear instance
         # (perturbed Q3 +2 %, Q6 +3 %, Q6 FP32 +5 %, profiles/r2_xtrilinear.md);
         # 2: every fused3 instance (the general-geometry kernel is
         # compute-bound: Q3 +0.6 %, Q6 -2.4 % on tiled storage,
@@ -144,7 +144,7 @@ class NativeCGRuntime:
         mode = os.environ.get("BDX_TILED", "1")
         esz = 8 if pb.dtype == torch.float64 else 4
         f3 = op.version == 3 and (mode == "2" or getattr(op, "x_trilinear", False))
-        self.tiled = (mode != "0" and (op.version in (4, 5) or f3)
+        self.tiled = (mode != "0" and (op.version == 5 or f3)
                       and (op.sy * op.sz * esz) % 16 == 0)
         self._latdT = None
         self._tbufs = []

@@ -2,8 +2,8 @@
 
 20 CG iterations on the headline meshes (Q3 at 300 M DoFs, Q6 at 500 M DoFs,
 FP64, qmode=1 GLL, one GPU), once with the production operator (fused5 at
-both degrees, and fused4 at Q3: Kronecker cores, lagged-x / interface-fold CG
-in the native runtime)
+both degrees: the Kronecker core, lagged-x / interface-fold CG in the native
+runtime)
 and once with the reference-structured `v1` kernel on stored geometry (G at
 every quadrature point, the layout of src/laplacian.hpp:105-114 and
 src/geometry_gpu.hpp:26-132; plain CG of src/cg.hpp:89-169).  Their iterate
@@ -42,7 +42,6 @@ def _solve(pb, u, kernel, geometry, nits):
 
 
 @pytest.mark.parametrize("degree,ndofs,kernel,prod", [(3, 300_000_000, "auto", "fused5"),
-                                                      (3, 300_000_000, "fused4", "fused4"),
                                                       (6, 500_000_000, "auto", "fused5")])
 def test_fullsize_cg_iterate_production_vs_stored_geometry(degree, ndofs, kernel, prod):
     torch.cuda.set_device(0)

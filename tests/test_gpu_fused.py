@@ -42,7 +42,7 @@ def _tol(dt):
 
 # (geometry, kernel version, affine fast path allowed)
 VARIANTS = [("otf", 1, True), ("stored", 1, True), ("otf", 2, True), ("otf", 2, False),
-            ("otf", 3, True), ("otf", 3, False), ("otf", 4, True), ("otf", 5, True)]
+            ("otf", 3, True), ("otf", 3, False), ("otf", 5, True)]
 
 
 def _skip_unsupported(pb, version):
@@ -103,11 +103,11 @@ def _cg_job(comm, nc, P, nreps, geometry, version=1, pert=0.1, runtime="native")
 
 @pytest.mark.parametrize("runtime", ["native", "python"])
 @pytest.mark.parametrize("pert", [0.0, 0.1])
-@pytest.mark.parametrize("version", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("version", [1, 2, 3, 5])
 @pytest.mark.parametrize("ranks", [2, 4, 8])
 def test_fused_partition_invariance_threaded(ranks, version, pert, runtime):
-    if version in (4, 5) and pert:
-        pytest.skip(f"fused{version} needs parallelepiped cells")
+    if version == 5 and pert:
+        pytest.skip("fused5 needs axis-aligned box cells")
     if version == 1 and runtime == "native":
         pytest.skip("the native runtime drives fused2/3")
     ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", version, pert, runtime)[0]
@@ -117,7 +117,7 @@ def test_fused_partition_invariance_threaded(ranks, version, pert, runtime):
             assert abs(a - b) <= 1e-11 * abs(b), (r, ref)
 
 
-@pytest.mark.parametrize("version", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("version", [1, 2, 3, 5])
 def test_fused_golden_and_mat_comp_16(version):
     if version != 3:  # qmode=0 (phi0 == I) is not a fused3 element
         nx = compute_mesh_size(1000, 3)
@@ -149,15 +149,13 @@ def test_fused3_cg_all_degrees(P, nc, pert):
     assert rel < 1e-10, rel
 
 
-@pytest.mark.parametrize("kernel", ["fused5", "fused4", "fused3", "fused2", "v1"])
+@pytest.mark.parametrize("kernel", ["fused5", "fused3", "fused2", "v1"])
 @pytest.mark.parametrize("nc,P,pert", [((4, 5, 7), 3, 0.0), ((3, 4, 5), 6, 0.1), ((5, 6, 6), 2, 0.0),
                                        ((9, 13, 10), 3, 0.0)])
 def test_random_coefficients_gpu(kernel, nc, P, pert):
     """Per-cell random kappa: GPU kernels vs the C++ CPU operator, and CG."""
     from benchmark_dolfinx_amd.driver import make_operator
     gpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "gpu", pert, "random")
-    if kernel == "fused4" and not (P == 3 and pert == 0.0):
-        pytest.skip("fused4: Q3 parallelepiped cells")
     if kernel == "fused5" and not (P >= 3 and pert == 0.0):
         pytest.skip("fused5: P >= 3 parallelepiped cells")
     cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", pert, "random")
@@ -182,19 +180,23 @@ def test_random_coefficients_gpu(kernel, nc, P, pert):
 @pytest.mark.parametrize("nc,coef", [((4, 8, 8), "constant"), ((8, 4, 16), "random"),
                                      ((16, 8, 4), "constant")])
 @pytest.mark.parametrize("shear", [0.5, 0.25])
-def test_fused4_sheared_parallelepipeds(nc, coef, shear):
-    """fused4's mixed Kronecker blocks (G01/G02/G12 != 0): sheared mesh whose
-    cells are parallelepipeds with a full Jacobian; action vs the C++ CPU
-    operator and CG vs the host CG."""
+def test_sheared_parallelepipeds_take_fused3_affine(nc, coef, shear):
+    """Parallelepipeds with a full Jacobian (G01/G02/G12 != 0, a sheared
+    mesh): fused5 refuses them and the auto choice is fused3's affine
+    instance; action vs the C++ CPU operator and CG vs the host CG."""
+    from benchmark_dolfinx_amd.driver import make_operator
     from benchmark_dolfinx_amd.models.fused import fused_supported
     gpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "gpu", 0.0, coef, shear)
     cpu = PoissonProblem(Comm(), nc, 3, 1, False, torch.float64, "cpu", 0.0, coef, shear)
-    assert gpu.all_affine and fused_supported(gpu, 4)
+    assert gpu.all_affine and not gpu.all_axis_aligned and not fused_supported(gpu, 5)
+    with pytest.raises(ValueError):
+        FusedLaplacianGPU(gpu, "otf", 5)
     rng = np.random.default_rng(11)
     u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
     yc = cpu.new_vector()
     MatFreeLaplacianCPU(cpu).apply(u64, yc)
-    op = FusedLaplacianGPU(gpu, "otf", 4)
+    op = make_operator(gpu)
+    assert op.name == "fused3" and op.geometry == "otf-affine", (op.name, op.geometry)
     yg = gpu.new_vector()
     op.apply(u64.to(gpu.device), yg)
     o = cpu.owned
@@ -210,10 +212,12 @@ def test_fused4_sheared_parallelepipeds(nc, coef, shear):
 
 
 def _cg_job_shear(comm, nc, nreps):
+    from benchmark_dolfinx_amd.driver import make_operator
     pb = PoissonProblem(comm, nc, 3, 1, False, torch.float64, "gpu", 0.0, "random", 0.5)
     u = pb.assemble_rhs()
     x = pb.new_vector()
-    op = FusedLaplacianGPU(pb, "otf", 4)
+    op = make_operator(pb)
+    assert op.name == "fused3", op.name
     DeviceCG(pb).solve(op, x, u, nreps)
     y = pb.new_vector()
     op.apply(u, y)
@@ -223,7 +227,7 @@ def _cg_job_shear(comm, nc, nreps):
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
-def test_fused4_sheared_partition_invariance(ranks):
+def test_sheared_partition_invariance(ranks):
     ref = run_threaded(1, _cg_job_shear, (8, 8, 16), 12)[0]
     got = run_threaded(ranks, _cg_job_shear, (8, 8, 16), 12)
     for r in got:
@@ -255,15 +259,21 @@ F5_CASES = [
 @pytest.mark.parametrize("coef", ["constant", "random"])
 @pytest.mark.parametrize("nc,P,qm,g,shear,dt", F5_CASES)
 def test_fused5_action_and_cg(nc, P, qm, g, shear, dt, coef):
-    """fused5 (nodal Kronecker core): axis-aligned boxes take the 2-array
-    instance, sheared parallelepipeds the 4-array one; action vs the C++ CPU
-    operator and CG vs the host CG."""
+    """fused5 (nodal Kronecker core) on axis-aligned boxes; sheared
+    parallelepipeds are refused by fused5 and run fused3's affine instance
+    (auto choice); action vs the C++ CPU operator and CG vs the host CG."""
+    from benchmark_dolfinx_amd.driver import make_operator
     from benchmark_dolfinx_amd.models.fused import fused_supported
     gpu = PoissonProblem(Comm(), nc, P, qm, g, dt, "gpu", 0.0, coef, shear)
     cpu = PoissonProblem(Comm(), nc, P, qm, g, torch.float64, "cpu", 0.0, coef, shear)
-    assert gpu.all_affine and fused_supported(gpu, 5)
-    op = FusedLaplacianGPU(gpu, "otf", 5)
-    assert op.affine_code == (2 if shear == 0.0 else 1)
+    assert gpu.all_affine and fused_supported(gpu, 5) == (shear == 0.0)
+    if shear == 0.0:
+        op = FusedLaplacianGPU(gpu, "otf", 5)
+        assert op.affine_code == 2
+    else:
+        op = make_operator(gpu)
+        if not (qm == 0 and not g):  # fused3 is the phi0 != I core (else fused2)
+            assert op.name == "fused3" and op.geometry == "otf-affine", (op.name, op.geometry)
     rng = np.random.default_rng(17)
     u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
     yc = cpu.new_vector()
@@ -289,7 +299,9 @@ def _cg_job_f5(comm, nc, P, nreps, shear):
     pb = PoissonProblem(comm, nc, P, 1, False, torch.float64, "gpu", 0.0, "random", shear)
     u = pb.assemble_rhs()
     x = pb.new_vector()
-    op = FusedLaplacianGPU(pb, "otf", 5)
+    from benchmark_dolfinx_amd.driver import make_operator
+    op = make_operator(pb)  # fused5 on the box, fused3 (affine) when sheared
+    assert op.name == ("fused5" if shear == 0.0 else "fused3"), op.name
     DeviceCG(pb).solve(op, x, u, nreps)
     y = pb.new_vector()
     op.apply(u, y)
@@ -311,7 +323,7 @@ def test_fused5_partition_invariance(ranks, shear, P, nc):
 
 # ---------------------------------------------------------------- x segments
 SEG_CASES = [  # version, P, perturb, dtype
-    (4, 3, 0.0, torch.float64), (5, 6, 0.0, torch.float64), (5, 4, 0.0, torch.float32),
+    (5, 3, 0.0, torch.float64), (5, 6, 0.0, torch.float64), (5, 4, 0.0, torch.float32),
     (2, 3, 0.2, torch.float64), (3, 3, 0.2, torch.float64), (3, 5, 0.0, torch.float32),
     (2, 2, 0.1, torch.float64)]
 
@@ -352,7 +364,7 @@ def test_fused_x_segments_cg_and_action(monkeypatch, version, P, pert, dt, nseg,
 
 @pytest.mark.parametrize("nseg", ["2", "4"])
 @pytest.mark.parametrize("ranks", [2, 4])
-@pytest.mark.parametrize("version,pert", [(4, 0.0), (5, 0.0), (3, 0.1)])
+@pytest.mark.parametrize("version,pert", [(5, 0.0), (3, 0.1)])
 def test_fused_x_segments_partition_invariance(monkeypatch, version, pert, nseg, ranks):
     monkeypatch.setenv("BDX_SEGMENTS", nseg)
     ref = run_threaded(1, _cg_job, (11, 14, 17), 3, 12, "otf", version, pert, "native")[0]

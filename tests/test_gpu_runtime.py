@@ -32,7 +32,7 @@ def _job(comm, nc, P, nreps, version, partition, pert=0.0, dtype=torch.float64,
         return None
     u = pb.assemble_rhs()
     x = pb.new_vector()
-    op = FusedLaplacianGPU(pb, "otf", version, affine=version in (4, 5) or pert == 0.0)
+    op = FusedLaplacianGPU(pb, "otf", version, affine=version == 5 or pert == 0.0)
     cg = DeviceCG(pb)
     cg.solve(op, x, u, nreps)
     cg.wait()
@@ -46,7 +46,7 @@ def _job(comm, nc, P, nreps, version, partition, pert=0.0, dtype=torch.float64,
 
 # meshes large enough that interior (ghost-free) tiles exist on every rank
 @pytest.mark.parametrize("version,P,nc", [(2, 3, (5, 22, 26)), (3, 3, (5, 22, 26)),
-                                          (4, 3, (5, 22, 26)), (5, 6, (3, 9, 10)),
+                                          (5, 3, (5, 22, 26)), (5, 6, (3, 9, 10)),
                                           (5, 4, (4, 14, 13))])
 @pytest.mark.parametrize("ranks", [2, 4, 8])
 def test_overlap_schedule_matches_one_rank(ranks, version, P, nc):
@@ -250,8 +250,8 @@ def _tiled_job(comm, nc, P, nreps, version, dtype, coef, shear=0.0, pert=0.0):
 
 
 @pytest.mark.parametrize("version,P,nc,dtype,coef", [
-    (4, 3, (6, 9, 14), torch.float64, "constant"),
-    (4, 3, (5, 13, 7), torch.float64, "random"),
+    (5, 3, (6, 9, 14), torch.float64, "constant"),
+    (5, 3, (5, 13, 7), torch.float64, "random"),
     (5, 6, (3, 5, 6), torch.float64, "random"),
     (5, 4, (4, 7, 9), torch.float64, "constant"),
     (5, 5, (3, 6, 5), torch.float64, "constant"),

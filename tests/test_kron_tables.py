@@ -1,4 +1,4 @@
-"""Host-side checks of the Kronecker-core tables (fused4 / fused5): the 1D
+"""Host-side checks of the Kronecker-core tables (fused5): the 1D
 matrices M = B^T W B, K = Dd^T W Dd, C = Dd^T W B packed by the HIP library's
 host entry points match numpy, and the Kronecker sum they define reproduces
 the dense element stiffness matrix of an affine cell (no GPU needed: the

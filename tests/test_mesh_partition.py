@@ -145,8 +145,9 @@ def test_parallelepiped_detection():
 
 def test_sheared_mesh_is_parallelepiped_with_full_jacobian():
     """The test-only shear map keeps every cell a parallelepiped (bitwise
-    check, needed by the fused4 kernel) while making the Jacobian full, so
-    the mixed geometry terms G01/G02/G12 are exercised."""
+    check) while making the Jacobian full, so the mixed geometry terms
+    G01/G02/G12 are exercised (fused3's affine instance; fused5 refuses
+    these cells)."""
     import torch
     from benchmark_dolfinx_amd.models.poisson import PoissonProblem
     from benchmark_dolfinx_amd.parallel.comm import Comm
