@@ -145,7 +145,7 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
         cg = DeviceCG(pb)
         cg.start(op, x, u)
         rt0 = getattr(op, "_rt", None)
-        if rt0 is not None and n > 1:
+        if rt0 is not None and n > 1 and rt0.transport in ("rccl", "thread"):
             # the first exchange and all-reduce of the runtime's own RCCL
             # communicator, bounded well below the run deadline: a peer that
             # never joins surfaces here as an error, not as a hung warmup

@@ -24,6 +24,29 @@ enum { kGeomStored = 0, kGeomOTF = 1 };
 // FP64 MFMA operand / accumulator vectors (v_mfma_f64_16x16x4f64: 4 results per lane)
 typedef double bdx_f64x4 __attribute__((ext_vector_type(4)));
 typedef double bdx_f64x2 __attribute__((ext_vector_type(2)));
+// FP32 (v_mfma_f32_16x16x4_f32: 4 results per lane, exact f32 fma chain)
+typedef float bdx_f32x4 __attribute__((ext_vector_type(4)));
+
+// 16 x 16 x 4 MFMA in T: A / B one T per lane (lane l: A[l & 15][k = l >> 4],
+// B[k = l >> 4][l & 15]); C / D 4 per lane.
+template <typename T> struct BdxMfmaAcc;
+template <> struct BdxMfmaAcc<double> { using type = bdx_f64x4; };
+template <> struct BdxMfmaAcc<float> { using type = bdx_f32x4; };
+__device__ __forceinline__ bdx_f64x4 bdx_mfma16x4(double a, double b, bdx_f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bdx_f32x4 bdx_mfma16x4(float a, float b, bdx_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// The result row of accumulator element r in lane group g (= lane >> 4) is
+// g + 4 r for FP64 and 4 g + r for FP32 (cdna_hip_programming.md §3).  Code
+// written for the FP64 map runs unchanged in FP32 when the row-carrying
+// operand's row m is taken from source row bdx_mfma_row<T>(m): then element r
+// of lane group g holds source row g + 4 r in both precisions.
+template <typename T>
+__device__ __forceinline__ constexpr int bdx_mfma_row(int m) {
+  return sizeof(T) == 8 ? m : (m >> 2) + 4 * (m & 3);
+}
 
 // Value of lane (l ^ 8) within each 16-lane row (DPP row_ror:8 = swap of the
 // row halves; two VALU moves per double, no LDS).

@@ -60,6 +60,9 @@ constexpr bool kF3Vec = true;
 constexpr bool kF3MfmaFrontY = false;
 constexpr bool kF3MfmaBackY = true;
 constexpr bool kF3MfmaBackZ = true;
+// the same three stages in FP32 (v_mfma_f32_16x16x4_f32; bdx_mfma_row maps
+// the FP32 accumulator rows onto the FP64 layout the stages are written for)
+constexpr bool kF3MfmaF32 = true;
 
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF, bool VEC = false>
@@ -96,9 +99,11 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads),
   // y / z contraction stages on the matrix pipe (see kF3Mfma*): FP64 cells
   // that are one wave each (Q6 qmode=1), x-trilinear and parallelepiped
   // instances (the general trilinear instance measured 1.3 % slower with them)
-  constexpr bool MFOK = sizeof(T) == 8 && NQ == 8 && ND == 7 && WAVELOCAL && AFF != 0;
+  constexpr bool MFOK = (sizeof(T) == 8 || kF3MfmaF32) && NQ == 8 && ND == 7 && WAVELOCAL &&
+                       AFF != 0;
   constexpr bool MFZ = kF3MfmaFrontZ && MFOK;
-  constexpr bool MFY = kF3MfmaFrontY && MFOK;
+  constexpr bool MFY = kF3MfmaFrontY && MFOK && sizeof(T) == 8;  // FP64 map only
+  using MAcc = typename BdxMfmaAcc<T>::type;
   constexpr bool MFBY = kF3MfmaBackY && MFOK;
   constexpr bool MFBZ = kF3MfmaBackZ && MFOK;
   // LDS work buffers of the contraction core: NBUFS buffers W[k][cell][i1][i2]
@@ -501,24 +506,23 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads),
       int ltid = tid;
       asm volatile("" : "+v"(ltid));  // lane roles and operands re-derived per layer, not hoisted
       const int mg = (ltid & 63) >> 4, mn = ltid & 15;
-      const T* __restrict__ arow = s_tab + (mn < NQ ? OFF_BR + mn * NP : OFF_DR + (mn - NQ) * NP);
-      const double a0 = arow[mg];
-      const double a1 = mg + 4 < ND ? arow[mg + 4] : 0.0;
+      const int mr = bdx_mfma_row<T>(mn);  // the table row this lane carries
+      const T* __restrict__ arow = s_tab + (mr < NQ ? OFF_BR + mr * NP : OFF_DR + (mr - NQ) * NP);
+      const T a0 = arow[mg];
+      const T a1 = mg + 4 < ND ? arow[mg + 4] : T(0);
       const int kb = mg + 4 < ND ? mg + 4 : ND - 1;  // k = 7: finite operand, zero row of A
       const T* __restrict__ ub = su + ycell * DZP + zcell;
       constexpr int NTL = (ND * ND + 15) / 16;
-      bdx_f64x4 acc[NTL];
+      MAcc acc[NTL];
 #pragma unroll
       for (int t = 0; t < NTL; ++t) {  // first k-step of every tile, then the second
         const int cc = t * 16 + mn < ND * ND ? t * 16 + mn : ND * ND - 1;
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, ub[(cc / ND) * PLP + (cc % ND) * DZP + mg],
-                                                      bdx_f64x4{0, 0, 0, 0}, 0, 0, 0);
+        acc[t] = bdx_mfma16x4(a0, ub[(cc / ND) * PLP + (cc % ND) * DZP + mg], MAcc{0, 0, 0, 0});
       }
 #pragma unroll
       for (int t = 0; t < NTL; ++t) {
         const int cc = t * 16 + mn < ND * ND ? t * 16 + mn : ND * ND - 1;
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, ub[(cc / ND) * PLP + (cc % ND) * DZP + kb],
-                                                      acc[t], 0, 0, 0);
+        acc[t] = bdx_mfma16x4(a1, ub[(cc / ND) * PLP + (cc % ND) * DZP + kb], acc[t]);
       }
 #pragma unroll
       for (int t = 0; t < NTL; ++t) {
@@ -804,21 +808,22 @@ BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
         constexpr int NE = NQ * ND, NTL = (NE + 15) / 16;
         auto pass = [&](int nks, const T* __restrict__ Wk0, const T* __restrict__ Wk1, T* __restrict__ Wout)
             __attribute__((always_inline)) {
-          double bk[4];
+          T bk[4];
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
             const int qy = (ks & 1) * 4 + mg;
-            bk[ks] = (ks < nks && mn < ND) ? s_tab[(ks < 2 ? OFF_BR : OFF_DR) + qy * NP + mn] : 0.0;
+            bk[ks] = (ks < nks && mn < ND) ? s_tab[(ks < 2 ? OFF_BR : OFF_DR) + qy * NP + mn] : T(0);
           }
           // k-step outer: the NTL independent accumulators interleave, so no
           // MFMA waits on the previous one's result
-          bdx_f64x4 acc[NTL];
+          MAcc acc[NTL];
           int aoff[NTL];
 #pragma unroll
           for (int t = 0; t < NTL; ++t) {
-            const int e = t * 16 + mn < NE ? t * 16 + mn : NE - 1;
+            const int m = t * 16 + bdx_mfma_row<T>(mn);
+            const int e = m < NE ? m : NE - 1;
             aoff[t] = offA(c, mg, e / ND) + (e - (e / ND) * ND);
-            acc[t] = bdx_f64x4{0, 0, 0, 0};
+            acc[t] = MAcc{0, 0, 0, 0};
           }
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
@@ -826,7 +831,7 @@ BDX_PRAGMA_UNROLL((QUnroll3G<T, NQ, AFF>::value))
 #pragma unroll
             for (int t = 0; t < NTL; ++t) {
               const T av = (ks < 2 ? Wk0 : Wk1)[aoff[t] + (ks & 1) * 4 * P1];
-              acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bk[ks], acc[t], 0, 0, 0);
+              acc[t] = bdx_mfma16x4(av, bk[ks], acc[t]);
             }
           }
           wave_order();  // every lane's reads are issued before the in-place writes
@@ -945,28 +950,28 @@ BDX_PRAGMA_UNROLL(2)
       int ltid = tid;
       asm volatile("" : "+v"(ltid));
       const int mg = (ltid & 63) >> 4, mn = ltid & 15;
-      double bk[4];
+      T bk[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int qz = (ks & 1) * 4 + mg;
-        bk[ks] = mn < ND ? s_tab[(ks < 2 ? OFF_BR : OFF_DR) + qz * NP + mn] : 0.0;
+        bk[ks] = mn < ND ? s_tab[(ks < 2 ? OFF_BR : OFF_DR) + qz * NP + mn] : T(0);
       }
       constexpr int NTL = (ND * ND + 15) / 16;
-      bdx_f64x4 acc[NTL];
+      MAcc acc[NTL];
       int aoff[NTL];
 #pragma unroll
       for (int t = 0; t < NTL; ++t) {
-        const int col = t * 16 + mn;
+        const int col = t * 16 + bdx_mfma_row<T>(mn);  // the (j, i) row this lane carries
         const int cc = col < ND * ND ? col : ND * ND - 1;
         aoff[t] = offA(c, cc / ND, mg) + (cc - (cc / ND) * ND);
-        acc[t] = bdx_f64x4{0, 0, 0, 0};
+        acc[t] = MAcc{0, 0, 0, 0};
       }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)  // k-step outer: independent accumulators interleave
 #pragma unroll
         for (int t = 0; t < NTL; ++t) {
           const T av = (ks < 2 ? W0 : W1)[aoff[t] + (ks & 1) * 4 * RP];
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bk[ks], acc[t], 0, 0, 0);
+          acc[t] = bdx_mfma16x4(av, bk[ks], acc[t]);
         }
       wave_order();  // every lane's C1 / C3 reads are issued before E overwrites W0
       if (mn < ND) {

@@ -48,6 +48,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -298,6 +299,78 @@ struct RcclTransport final : Transport {
   }
 };
 
+// Emulated link (one rank of an N-rank run alone on this device: bench /
+// scripts/emulate_rank.py).  Every exchange is a device copy of the send
+// buffer into the receive buffer by a few workgroups (RCCL's p2p kernels
+// occupy a few CUs the same way) that hold their CUs until the modelled link
+// time has passed: max over peers of the bytes to or from that peer /
+// link_gbps (one xGMI link per peer) + lat_us.  An all-reduce is a single
+// workgroup held for allreduce_us.  The copies carry the rank's own face
+// data, not a peer's: the emulation is for timing the schedule, not for
+// results.  Bounded: each workgroup waits on the 100 MHz constant clock from
+// its own start, nothing else.
+__global__ void __launch_bounds__(256)
+    bdx_link_emu_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16,
+                        int64_t ticks) {
+  const long long t0 = wall_clock64();
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    dst[i] = src[i];
+  if (threadIdx.x == 0) {
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  }
+  __syncthreads();
+}
+
+struct LinkEmuTransport final : Transport {
+  int nranks = 1;
+  double link_gbps = 50.0, lat_us = 10.0, allreduce_us = 20.0;
+  int nwg = 8;
+  static double env(const char* k, double d) {
+    const char* e = std::getenv(k);
+    return e ? std::atof(e) : d;
+  }
+  LinkEmuTransport() {
+    link_gbps = env("BDX_EMU_LINK_GBPS", 50.0);
+    lat_us = env("BDX_EMU_LINK_LAT_US", 10.0);
+    allreduce_us = env("BDX_EMU_ALLREDUCE_US", 20.0);
+    nwg = static_cast<int>(env("BDX_EMU_LINK_WG", 8));
+    if (nwg < 1) nwg = 1;
+  }
+  // modelled link time of one exchange, microseconds
+  double exchange_us(const std::vector<int64_t>& scnt, const std::vector<int64_t>& rcnt,
+                     int esize) const {
+    int64_t worst = 0;
+    for (size_t p = 0; p < scnt.size() && p < rcnt.size(); ++p)
+      worst = std::max(worst, std::max(scnt[p], rcnt[p]) * esize);
+    if (worst == 0) return 0.0;
+    return worst / (link_gbps * 1e3) + lat_us;  // bytes / (1e3 link_gbps) = us
+  }
+  int exchange(const void* sbuf, const std::vector<int64_t>& scnt,
+               const std::vector<int64_t>& soff, void* rbuf, const std::vector<int64_t>& rcnt,
+               const std::vector<int64_t>& roff, int esize, hipStream_t st) override {
+    (void)soff;
+    (void)roff;
+    int64_t ns = 0, nr = 0;
+    for (int64_t c : scnt) ns += c;
+    for (int64_t c : rcnt) nr += c;
+    const double us = exchange_us(scnt, rcnt, esize);
+    if (us <= 0.0) return 0;
+    const int64_t n16 = std::min(ns, nr) * esize / 16;
+    hipLaunchKernelGGL(bdx_link_emu_kernel, dim3(nwg), dim3(256), 0, st,
+                       static_cast<const uint4*>(sbuf), static_cast<uint4*>(rbuf), n16,
+                       static_cast<int64_t>(us * 100.0));
+    return static_cast<int>(hipGetLastError());
+  }
+  int allreduce_sum(double*, int, hipStream_t st) override {
+    hipLaunchKernelGGL(bdx_link_emu_kernel, dim3(1), dim3(256), 0, st, nullptr, nullptr,
+                       int64_t{0}, static_cast<int64_t>(allreduce_us * 100.0));
+    return static_cast<int>(hipGetLastError());
+  }
+  bool capturable() const override { return true; }
+  int ranks() const override { return nranks; }
+};
+
 // Single rank: no communication at all.
 struct NoTransport final : Transport {
   int exchange(const void*, const std::vector<int64_t>&, const std::vector<int64_t>&, void*,
@@ -438,6 +511,15 @@ struct LoopBase {
   // default stream torch may be using); ordered against the caller's stream
   // `ext` with events at the start and end of every iterate()
   hipStream_t st = nullptr, cs = nullptr, ext = nullptr;
+  // Split schedule, interior launch: on st (si == nullptr), or on its own
+  // stream si whose CU mask leaves `reserve` CUs to the comm stream's chain
+  // (BDX_SPLIT=mask; make_interior_stream).  cu_mask_cs: cs was created with
+  // the complementary mask (BDX_SPLIT=maskr: the chain on the reserved CUs
+  // only).
+  hipStream_t si = nullptr;
+  hipEvent_t ev_int = nullptr;
+  int reserve = 0;
+  std::vector<uint32_t> mask_si, mask_cs;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_rev = nullptr;
   // halo: owned lower faces <-> ghost planes (parallel/halo.py layout), on
   // the storage layout `wlatd` describes
@@ -474,6 +556,8 @@ struct LoopBase {
     for (hipEvent_t e : tev) hipEventDestroy(e);
     for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_rev, ev_batch[0], ev_batch[1]})
       if (e) hipEventDestroy(e);
+    if (si) hipStreamDestroy(si);
+    if (ev_int) hipEventDestroy(ev_int);
     if (st) hipStreamDestroy(st);
     if (cs) hipStreamDestroy(cs);
     if (pf_scal) hipFree(pf_scal);
@@ -491,6 +575,53 @@ struct LoopBase {
 
   void mark(int id, hipStream_t s) {
     if (prof) (void)hipEventRecord(pev[id], s);
+  }
+
+  // The interior launch's stream of the split schedule (BDX_SPLIT):
+  //   prio  (default) the compute stream st; the comm stream has the
+  //         device's greatest priority;
+  //   mask  its own stream si whose CU mask excludes BDX_SPLIT_RESERVE CUs
+  //         (default 16), so the comm stream's chain -- RCCL kernels,
+  //         boundary tiles, ghost fold -- always finds free CUs instead of
+  //         queueing behind the interior grid's workgroups;
+  //   maskr as mask, and the comm stream is confined to the reserved CUs.
+  // The reserved CUs are mask bits 0 .. reserve-1, which the hardware deals
+  // round-robin over the XCDs (csrc/micro/dispatch_prio.hip census).
+  int make_interior_stream() {
+    const char* e = std::getenv("BDX_SPLIT");
+    const std::string mode = e ? e : "prio";
+    if (mode == "prio" || mode.empty()) return 0;
+    if (mode != "mask" && mode != "maskr") return static_cast<int>(hipErrorInvalidValue);
+    int dev = 0, ncu = 0;
+    BDX_CHECK(hipGetDevice(&dev));
+    BDX_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const char* r = std::getenv("BDX_SPLIT_RESERVE");
+    reserve = r ? std::atoi(r) : 16;
+    if (reserve < 1 || reserve >= ncu) return static_cast<int>(hipErrorInvalidValue);
+    const int words = (ncu + 31) / 32;
+    mask_si.assign(words, 0u);
+    mask_cs.assign(words, 0u);
+    for (int b = 0; b < ncu; ++b) (b < reserve ? mask_cs : mask_si)[b / 32] |= 1u << (b % 32);
+    BDX_CHECK(hipExtStreamCreateWithCUMask(&si, static_cast<uint32_t>(words), mask_si.data()));
+    BDX_CHECK(hipEventCreateWithFlags(&ev_int, hipEventDisableTiming));
+    if (mode == "maskr") {
+      BDX_CHECK(hipStreamDestroy(cs));
+      cs = nullptr;
+      BDX_CHECK(hipExtStreamCreateWithCUMask(&cs, static_cast<uint32_t>(words), mask_cs.data()));
+      BDX_CHECK(hipStreamGetPriority(cs, &prio_cs));
+    }
+    return 0;
+  }
+  // interior launch `f(stream)` of the split schedule on si or st; st
+  // continues after it (the caller then joins the comm stream)
+  template <typename F>
+  int interior(F&& f) {
+    if (!si) return f(st);
+    BDX_CHECK(hipStreamWaitEvent(si, ev_fork, 0));
+    if (int rc = f(si)) return rc;
+    BDX_CHECK(hipEventRecord(ev_int, si));
+    BDX_CHECK(hipStreamWaitEvent(st, ev_int, 0));
+    return 0;
   }
 
   // Streams, events, halo tables and the transport (every runtime kind).
@@ -552,6 +683,10 @@ struct LoopBase {
         t->g = g;
       }
       t->rank = r;
+      tr = std::move(t);
+    } else if (transport == 3 && n > 1) {  // emulated links (one rank alone)
+      auto t = std::make_unique<LinkEmuTransport>();
+      t->nranks = n;
       tr = std::move(t);
     } else {  // single rank: no communication
       tr = std::make_unique<NoTransport>();
@@ -891,8 +1026,12 @@ struct CGRuntime final : LoopBase {
       if ((rc = halo_reverse_send(y, cs))) return rc;
       BDX_CHECK(hipEventRecord(ev_rev, cs));
       mark(kMRevEnd, cs);
-      if ((rc = op(rect_a, st))) return rc;
-      mark(kMOpA, st);
+      if ((rc = interior([&](hipStream_t s) {
+             const int r2 = op(rect_a, s);
+             mark(kMOpA, s);
+             return r2;
+           })))
+        return rc;
       BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
       if ((rc = halo_reverse_add(y, st))) return rc;
       mark(kMJoin, st);
@@ -994,14 +1133,14 @@ struct CGRuntime final : LoopBase {
       return rc;
     };
     hipEvent_t e[5] = {};
-    for (auto& x : e) BDX_CHECK(hipEventCreate(&x));
-    struct Free {
+    struct Free {  // before the creation loop: a failed create leaks nothing
       hipEvent_t* e;
       ~Free() {
         for (int i = 0; i < 5; ++i)
           if (e[i]) hipEventDestroy(e[i]);
       }
     } fr{e};
+    for (auto& x : e) BDX_CHECK(hipEventCreate(&x));
     auto ms = [&](int a, int b) {
       float v = 0.f;
       (void)hipEventElapsedTime(&v, e[a], e[b]);
@@ -1121,8 +1260,12 @@ struct DofCGRuntime final : LoopBase {
       if ((rc = halo_reverse_send(y, cs))) return rc;
       BDX_CHECK(hipEventRecord(ev_rev, cs));
       mark(kMRevEnd, cs);
-      if ((rc = run(inner, cfg.n_inner, partials, k, first, xlag, st))) return rc;
-      mark(kMOpA, st);
+      if ((rc = interior([&](hipStream_t s) {
+             const int r2 = run(inner, cfg.n_inner, partials, k, first, xlag, s);
+             mark(kMOpA, s);
+             return r2;
+           })))
+        return rc;
       BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
       if ((rc = halo_reverse_add(y, st))) return rc;
       mark(kMJoin, st);
@@ -1261,6 +1404,7 @@ LoopBase* create(const int64_t* latd, const int64_t* own, const int* iparams, do
     std::memcpy(rt->rect_r1, r1, sizeof(r1));
     std::memcpy(rt->rect_r2, r2, sizeof(r2));
     rt->split = true;
+    if (rt->make_interior_stream()) return nullptr;
   }
   return rt.release();
 }
@@ -1317,6 +1461,7 @@ LoopBase* create_dofmap(const int64_t* latd, const int* iparams, int64_t nvec, d
                       group_id))
     return nullptr;
   rt->split = overlap && rt->halo && c.n_outer > 0;
+  if (rt->split && rt->make_interior_stream()) return nullptr;
   return rt.release();
 }
 

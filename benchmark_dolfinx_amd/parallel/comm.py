@@ -175,6 +175,48 @@ class ThreadComm(Comm):
         return out
 
 
+class EmulatedRankComm(Comm):
+    """Rank `rank` of an N-rank run, alone on this device (experiments:
+    scripts/emulate_rank.py).
+
+    The problem is that rank's block of the N-rank partition, ghost planes
+    included, so the operator and the native runtime's split schedule run
+    exactly as on the rank of a real N-GPU run; the native runtime replaces
+    RCCL by modelled link times (runtime.hip LinkEmuTransport).  Host-side
+    collectives are local no-ops: all-reduces return the rank's own values
+    and all-to-alls deliver zeros, so norms are this rank's, not the global
+    problem's -- for timing the schedule, not for results.
+    """
+
+    def __init__(self, rank: int, size: int):
+        self.enabled = True
+        self.rank = rank
+        self.size = size
+        self.backend = "emulated"
+
+    @property
+    def device(self) -> torch.device:
+        if torch.cuda.is_available():
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def allreduce_(self, t, op: str = "sum", async_op: bool = False):
+        return _Done() if async_op else None
+
+    def allreduce_scalar(self, v: float, op: str = "sum") -> float:
+        return float(v)
+
+    def alltoallv(self, out, inp, out_splits, in_splits, async_op: bool = False):
+        out.zero_()
+        return _Done() if async_op else None
+
+    def barrier(self):
+        return None
+
+    def gather_objects(self, obj):
+        return [obj] * self.size
+
+
 def run_threaded(size: int, fn, *args, emulate: str = "thread", **kwargs):
     """Run fn(comm, *args) on `size` in-process ranks; returns the per-rank results."""
     import threading

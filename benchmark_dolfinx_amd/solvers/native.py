@@ -87,9 +87,14 @@ class NativeCGRuntime:
             # pick up a stale group of a runtime that was not closed yet
         elif comm.backend == "nccl":
             transport = 1
+        elif comm.backend == "emulated":  # EmulatedRankComm: modelled links
+            transport = 3
+            halo.buf_a.zero_()  # the emulated copies move finite data only
+            halo.buf_b.zero_()
         else:
             transport = -1
-        self.transport = {0: "none", 1: "rccl", 2: "thread"}.get(transport, "unsupported")
+        self.transport = {0: "none", 1: "rccl", 2: "thread", 3: "emulated"}.get(
+            transport, "unsupported")
         self.upart = torch.zeros(self.lib.bdx_hip_partials_size(), dtype=torch.float64,
                                  device=pb.device)
         self.x = cg.x

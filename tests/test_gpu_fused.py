@@ -417,6 +417,38 @@ def test_fused3_x_trilinear_instance(nc, P, dt, coef):
     assert make_operator(sh).geometry == "otf-general"
 
 
+@pytest.mark.parametrize("P,nc", [(6, (3, 4, 5)), (6, (2, 5, 3)), (7, (2, 3, 4))])
+@pytest.mark.parametrize("pert", [0.0, 0.2])
+@pytest.mark.parametrize("coef", ["constant", "random"])
+def test_fused3_fp32_q6_q7(P, nc, pert, coef):
+    """fused3 in FP32 at P = 6 (y / z stages on v_mfma_f32_16x16x4_f32 for the
+    parallelepiped and x-trilinear instances) and P = 7 (VALU): action vs the
+    FP64 C++ CPU operator, CG vs the FP64 host CG (FP32 tolerances)."""
+    gpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float32, "gpu", pert, coef)
+    _skip_unsupported(gpu, 3)
+    cpu = PoissonProblem(Comm(), nc, P, 1, False, torch.float64, "cpu", pert, coef)
+    op = FusedLaplacianGPU(gpu, "otf", 3)
+    assert op.affine_code == (1 if pert == 0.0 else 2)
+    rng = np.random.default_rng(21)
+    u64 = torch.from_numpy(rng.standard_normal(cpu.lat.shape))
+    yc = cpu.new_vector()
+    MatFreeLaplacianCPU(cpu).apply(u64, yc)
+    yg = torch.full(gpu.lat.shape, float("nan"), dtype=torch.float32, device=gpu.device)
+    op.apply(u64.to(gpu.device, torch.float32), yg)
+    o = cpu.owned
+    yg = yg.double().cpu()
+    assert torch.isfinite(o(yg)).all()
+    err = (o(yg) - o(yc)).abs().max().item()
+    assert err <= _tol(torch.float32) * 50 * max(1.0, yc.abs().max().item()), err
+    xg = gpu.new_vector()
+    DeviceCG(gpu).solve(op, xg, gpu.assemble_rhs(), 15)
+    xc = cpu.new_vector()
+    cg_solve(MatFreeLaplacianCPU(cpu), cpu, xc, cpu.assemble_rhs(), 15)
+    rel = (o(xg.double().cpu()) - o(xc)).abs().max().item() / xc.abs().max().item()
+    assert rel < 2e-4, rel
+    op.close()
+
+
 @pytest.mark.parametrize("ranks", [2, 4])
 def test_fused3_x_trilinear_partition_invariance(ranks):
     ref = run_threaded(1, _cg_job, (6, 7, 9), 3, 15, "otf", 3, 0.15)[0]
