@@ -55,6 +55,16 @@ constexpr int kF5Waves = 2;
 // 16-byte staging loads / stores (the VEC instance, lap_fused5_kernel)
 constexpr bool kF5Vec = true;
 
+// Slab pitches of the FP64 ND = 7 (Q6) instance congruent to 7 mod 16 words:
+// the x-pass and p.Ap reads put 7 lanes on each slab row, so a 16-lane group
+// of a ds_read2_b64 then covers 16 consecutive banks instead of colliding on
+// the next row's first ones (scripts/lds_bank_f5.py: 168 of the 546 modelled
+// conflict cycles per layer and workgroup removed; LDS 54 -> 70 KB, still 2
+// workgroups per CU).  Other instances keep the odd pitch DZ | 1 (Q3's LDS
+// budget holds exactly 4 workgroups per CU).
+constexpr bool kF5Pad7 = true;
+constexpr int f5_pad7(int n) { return n + ((7 - n % 16) + 16) % 16; }
+
 // table layout: M, K, C, C^T as 8 x 8 row-major blocks, then the even-odd
 // forms of M and K (4 x 4 blocks at kF5EO + 32 id: E, then O at + 16)
 constexpr int kF5Stride = 8;
@@ -108,7 +118,9 @@ struct F5Shape {
   static constexpr int WB0 = 2 * ARR;  // arrays 0 (Kx u / zM) and 1 (Mx u / zK)
   static constexpr int WB = WB0 > CPW * PC ? WB0 : CPW * PC;  // per-wave buffer
   static constexpr int DY = TY * P + 1, DZ = TZ * P + 1, PL = DY * DZ;
-  static constexpr int DZP = DZ | 1, PLP = DY * DZP;
+  static constexpr bool PAD7 = kF5Pad7 && sizeof(T) == 8 && ND == 7;
+  static constexpr int DZP = PAD7 ? f5_pad7(DZ) : (DZ | 1);
+  static constexpr int PLP = PAD7 ? f5_pad7(DY * DZP) : DY * DZP;
 };
 
 // Does a tile row's own part split into whole 16-byte vectors (the VEC instance)?

@@ -62,12 +62,12 @@ def shape(ND: int):
 
 
 def sites(ND: int, DZP: int | None = None, NDP: int | None = None, RP: int | None = None,
-          wave: int = 0):
+          PLP: int | None = None, wave: int = 0):
     """(site, kind, {lane: element}) for one layer of wave `wave` (FP64)."""
     P, CPW, TY, TZ = shape(ND)
     DY, DZ = TY * P + 1, TZ * P + 1
     DZP = DZP or (DZ | 1)
-    PLP = DY * DZP
+    PLP = PLP or DY * DZP
     VW = 2
     SLOTS = (ND + VW - 1) // VW
     NDP = NDP or (SLOTS if SLOTS % 2 else SLOTS + 1) * VW
@@ -188,3 +188,7 @@ def report(ND: int, **kw):
 if __name__ == "__main__":
     for ND in (4, 7):
         report(ND)
+    # slab pitches congruent to 7 mod 16 words: a 16-lane group of the x-pass
+    # and p.Ap reads (7 lanes per row) covers 16 consecutive banks
+    report(7, DZP=23, PLP=311)
+    report(6, DZP=23 if 2 * 5 + 1 <= 23 else None)
