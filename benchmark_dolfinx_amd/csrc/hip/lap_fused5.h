@@ -55,14 +55,14 @@ constexpr int kF5Waves = 2;
 // 16-byte staging loads / stores (the VEC instance, lap_fused5_kernel)
 constexpr bool kF5Vec = true;
 
-// Slab pitches of the FP64 ND = 7 (Q6) instance congruent to 7 mod 16 words:
-// the x-pass and p.Ap reads put 7 lanes on each slab row, so a 16-lane group
-// of a ds_read2_b64 then covers 16 consecutive banks instead of colliding on
-// the next row's first ones (scripts/lds_bank_f5.py: 168 of the 546 modelled
-// conflict cycles per layer and workgroup removed; LDS 54 -> 70 KB, still 2
-// workgroups per CU).  Other instances keep the odd pitch DZ | 1 (Q3's LDS
-// budget holds exactly 4 workgroups per CU).
-constexpr bool kF5Pad7 = true;
+// Slab pitches of the FP64 ND = 7 (Q6) instance congruent to 7 mod 16 words
+// (switch): the x-pass and p.Ap reads put 7 lanes on each slab row, so a
+// 16-lane group of a ds_read2_b64 then covers 16 consecutive banks instead of
+// colliding on the next row's first ones (scripts/lds_bank_f5.py: 168 of the
+// 546 modelled conflict cycles per layer and workgroup).  Measured off: bank
+// conflicts -10 %, no fewer LDS waits, 0.4 % slower (the larger pitch breaks
+// ds_read2_b64 pairing, +4 % LDS instructions; profiles/r5_kernel_ab.md).
+constexpr bool kF5Pad7 = false;
 constexpr int f5_pad7(int n) { return n + ((7 - n % 16) + 16) % 16; }
 
 // table layout: M, K, C, C^T as 8 x 8 row-major blocks, then the even-odd
