@@ -735,11 +735,16 @@ static __global__ void __launch_bounds__(256)
 
 // CG update of the dofmap path: alpha = s[rn] / s[pap]; r -= alpha y over
 // every local dof, r.r over the owned ones, y = 0 for the next operator.
-// 16-byte vectors (and W flag bytes) per thread; block 0 takes the tail.
-// Non-temporal r / y loads and stores (a pure stream): update pass Q3 2.29 ->
-// 2.00 ms, Q6 3.07 -> 2.74, +1.5 % / +2-4 % GDoF/s same box
-// (profiles/r4_update_pass_ab.txt).
-template <typename T>
+// 16-byte vectors (and W flag bytes); block 0 takes the tail.  Non-temporal
+// r / y loads and stores (a pure stream): update pass Q3 2.29 -> 2.00 ms, Q6
+// 3.07 -> 2.74, +1.5 % / +2-4 % GDoF/s same box (profiles/r4_update_pass_ab.txt).
+// Round 5: U vectors per thread per pass of the grid-stride loop, every load
+// of a pass issued before any arithmetic (the tiled update pass's form,
+// fused_common.hip): with one vector per thread and pass the loop kept a
+// single 16-byte r / y pair in flight per thread and ran 1.56 ms on one box
+// and 2.17 ms on another at Q3 (profiles/r5_dofmap_update.md).
+constexpr int kDofUpdU = 4;
+template <typename T, int U>
 __global__ void __launch_bounds__(256)
     dofmap_cg_update_kernel(int64_t n, const unsigned char* __restrict__ flags, T* __restrict__ r,
                             T* __restrict__ y, const double* __restrict__ scal, int rn_slot,
@@ -751,16 +756,31 @@ __global__ void __launch_bounds__(256)
   typedef unsigned char F __attribute__((ext_vector_type(W)));
   double acc = 0.0;
   const int64_t nv = n / W;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv;
-       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const V rn = __builtin_nontemporal_load(reinterpret_cast<const V*>(r + v * W)) -
-                 alpha * __builtin_nontemporal_load(reinterpret_cast<const V*>(y + v * W));
-    const F fl = *reinterpret_cast<const F*>(flags + v * W);
-    __builtin_nontemporal_store(rn, reinterpret_cast<V*>(r + v * W));
-    __builtin_nontemporal_store(V(0), reinterpret_cast<V*>(y + v * W));
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * (256 * U);
+  for (int64_t vb = static_cast<int64_t>(blockIdx.x) * (256 * U) + threadIdx.x; vb < nv;
+       vb += stride) {
+    V vr[U], vy[U];
+    F fl[U];
 #pragma unroll
-    for (int w = 0; w < W; ++w)
-      if (fl[w] & 2u) acc += static_cast<double>(rn[w]) * static_cast<double>(rn[w]);
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = vb + u * 256;
+      if (v < nv) {
+        vr[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(r + v * W));
+        vy[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(y + v * W));
+        fl[u] = *reinterpret_cast<const F*>(flags + v * W);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = vb + u * 256;
+      if (v >= nv) break;
+      const V rn = vr[u] - alpha * vy[u];
+      __builtin_nontemporal_store(rn, reinterpret_cast<V*>(r + v * W));
+      __builtin_nontemporal_store(V(0), reinterpret_cast<V*>(y + v * W));
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        if (fl[u][w] & 2u) acc += static_cast<double>(rn[w]) * static_cast<double>(rn[w]);
+    }
   }
   if (blockIdx.x == 0) {
     for (int64_t i = nv * W + threadIdx.x; i < n; i += blockDim.x) {
@@ -876,10 +896,11 @@ int launch_dofmap_geometry(int ncells, const int* cverts, const T* coords, const
   extern "C" int bdx_dofmap_cg_update_##SUF(int64_t n, const unsigned char* flags, T* r, T* y,    \
                                             const double* scal, int rn_slot, int pap_slot,        \
                                             double* partials, int* nblocks, hipStream_t st) {     \
-    const int64_t want = (n / (16 / static_cast<int64_t>(sizeof(T))) + 1023) / 1024;              \
+    const int64_t want = (n / (16 / static_cast<int64_t>(sizeof(T))) + 256 * kDofUpdU - 1) /      \
+                         (256 * kDofUpdU);                                                        \
     const int g = static_cast<int>(want < kDofMaxBlocks ? (want > 0 ? want : 1) : kDofMaxBlocks); \
-    dofmap_cg_update_kernel<T><<<g, 256, 0, st>>>(n, flags, r, y, scal, rn_slot, pap_slot,        \
-                                                  partials);                                      \
+    dofmap_cg_update_kernel<T, kDofUpdU><<<g, 256, 0, st>>>(n, flags, r, y, scal, rn_slot,        \
+                                                            pap_slot, partials);                  \
     *nblocks = g;                                                                                 \
     return static_cast<int>(hipGetLastError());                                                   \
   }                                                                                               \
