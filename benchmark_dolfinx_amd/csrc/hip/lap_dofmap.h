@@ -733,6 +733,9 @@ static __global__ void __launch_bounds__(256)
   *e = (first[d] == pos0 + static_cast<unsigned>(t)) ? (d | static_cast<int>(0x80000000u)) : d;
 }
 
+// Vectors per thread and pass of dofmap_cg_update_kernel (below).
+constexpr int kDofUpdU = 4;
+
 // CG update of the dofmap path: alpha = s[rn] / s[pap]; r -= alpha y over
 // every local dof, r.r over the owned ones, y = 0 for the next operator.
 // 16-byte vectors (and W flag bytes); block 0 takes the tail.  Non-temporal
@@ -743,7 +746,6 @@ static __global__ void __launch_bounds__(256)
 // fused_common.hip): with one vector per thread and pass the loop kept a
 // single 16-byte r / y pair in flight per thread and ran 1.56 ms on one box
 // and 2.17 ms on another at Q3 (profiles/r5_dofmap_update.md).
-constexpr int kDofUpdU = 4;
 template <typename T, int U>
 __global__ void __launch_bounds__(256)
     dofmap_cg_update_kernel(int64_t n, const unsigned char* __restrict__ flags, T* __restrict__ r,

@@ -63,6 +63,16 @@ constexpr bool kF5Vec = true;
 // conflicts -10 %, no fewer LDS waits, 0.4 % slower (the larger pitch breaks
 // ds_read2_b64 pairing, +4 % LDS instructions; profiles/r5_kernel_ab.md).
 constexpr bool kF5Pad7 = false;
+
+// Late prefetch (switch): issue the next layer's loads after the z pass
+// instead of at the top of the layer, so their registers are not live during
+// the x and z passes; with it the FP64 ND = 7 (Q6) CG instance is compiled
+// for 3 waves / SIMD (LDS admits 3 workgroups per CU).
+constexpr bool kF5Late = false;
+template <typename T, int ND, int MODE>
+constexpr bool f5_late() { return kF5Late && sizeof(T) == 8 && ND == 7 && MODE == 1; }
+template <typename T, int ND, int MODE>
+constexpr int f5_waves() { return f5_late<T, ND, MODE>() ? 3 : kF5Waves; }
 constexpr int f5_pad7(int n) { return n + ((7 - n % 16) + 16) % 16; }
 
 // table layout: M, K, C, C^T as 8 x 8 row-major blocks, then the even-odd
@@ -135,7 +145,7 @@ constexpr bool f5_vec_shape() {
 // (An MFMA form of the three passes lost to this VALU core at Q6 in both
 // precisions: profiles/r2_fused5_mfma.md, profiles/r3_mfma.md.)
 template <typename T, int ND, int MODE, bool VEC = false>
-__global__ void __launch_bounds__((F5Shape<T, ND>::NT), kF5Waves)
+__global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()))
     lap_fused5_kernel(Fused2Args<T> A, const T* __restrict__ tabd) {
   using S = F5Shape<T, ND>;
   constexpr int P = S::P, CPW = S::CPW, TY = S::TY, TZ = S::TZ;
@@ -499,6 +509,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), kF5Waves)
     __syncthreads();
 
     // ---- prefetch the next layer (planes 1..P of layer cx+1, vertex plane cx+2)
+    constexpr bool LATE = f5_late<T, ND, MODE>();
     const int64_t lnext = static_cast<int64_t>(cx + 1) * P * A.ps;
     const T* __restrict__ un_r = A.u + lnext;
     const T* __restrict__ un_p = A.pold + lnext;
@@ -511,6 +522,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), kF5Waves)
     // next layer's cell coefficient rides with the prefetch: a load consumed
     // in the same layer would make the wave wait for the whole batch
     T kc_nxt = kc_cur;
+    auto issue_prefetch = [&]() __attribute__((always_inline)) {
     if (A.kc && !last && cell_on) kc_nxt = A.kc[static_cast<int64_t>(cx + 1) * kc_ps + kc_cell];
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
@@ -565,6 +577,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), kF5Waves)
       pf_v[k] = T(0);
       if (!last && v_off[k] >= 0) pf_v[k] = A.xv[static_cast<int64_t>(cx + 2) * A.vps + v_off[k]];
     }
+    };
+    if constexpr (!LATE) issue_prefetch();
 
     const T* __restrict__ su = s_u[cur];
     const T* __restrict__ sX = s_X[cur];
@@ -653,6 +667,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), kF5Waves)
       }
       wave_sync();
     }
+
+    if constexpr (LATE) issue_prefetch();
 
     // ------------------------------------------------ y pass: lane (i, k) = (la, lb)
     T ye[ND];

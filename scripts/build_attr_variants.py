@@ -9,7 +9,6 @@ production library): libbdx_hip_<name>.so from a scratch copy of the sources.
 
   python scripts/build_attr_variants.py d1 d4 d6
 """
-import re
 import shutil
 import subprocess
 import sys
@@ -29,9 +28,10 @@ def patch(src: str, name: str) -> str:
         old = "        if (last || !(m & (1 << 21))) continue;\n"
         assert src.count(old) == 2, src.count(old)
         src = src.replace(old, "        continue;\n")
-        old = "      if (!last && (st_meta[k] & kValid)) {\n        if (BDX_OOB(lnext + st_goff[k], A.vsize, \"f5 prefetch\")) continue;"
+        tail = "\n        if (BDX_OOB(lnext + st_goff[k], A.vsize, \"f5 prefetch\")) continue;"
+        old = "      if (!last && (st_meta[k] & kValid)) {" + tail
         assert src.count(old) == 1
-        src = src.replace(old, "      if (false) {\n        if (BDX_OOB(lnext + st_goff[k], A.vsize, \"f5 prefetch\")) continue;")
+        src = src.replace(old, "      if (false) {" + tail)
     if name == "d6":
         old = "          if (red || (pl == P && !glast)) continue;"
         assert src.count(old) == 1
