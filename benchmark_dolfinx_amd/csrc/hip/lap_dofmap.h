@@ -46,6 +46,16 @@
 #include "lap_v1.h"
 
 enum { kDofAction = 0, kDofCG = 1 };
+
+// Pipeline schedule (switches kept with their A/B records): kDofEarly issues
+// the next cell's gathers (and the dofs of the cell after it) as soon as the
+// element stage has consumed the current ones, and the next cell's stored G
+// as soon as the F stage has moved the current G to LDS, so both are in
+// flight for a whole iteration instead of from the end of one to the start /
+// middle of the next (stored-G instances).  kDofGnt streams G non-temporally (66.6 GB per apply
+// at Q3, read once: kept out of the caches that the gathers reuse).
+constexpr bool kDofEarly = true;
+constexpr bool kDofGnt = true;
 typedef unsigned bdx_u32x2 __attribute__((ext_vector_type(2)));
 
 template <int NQ>
@@ -103,6 +113,12 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   constexpr int ND3 = ND * ND * ND, NQ3 = NQ * NQ * NQ;
   constexpr bool IDENT = ND == NQ;  // qmode 0, GLL: phi0 = I (quirk Q5 guarantees it)
   constexpr bool GPREF = GEOM == kGeomStored && S::GPREF;
+  // early issue: instances with prefetched stored G.  On-the-fly geometry is
+  // register-bound (the early gathers push its Q5 / Q6 CG instances to 1
+  // wave / SIMD); with G loaded where it is used (NQ >= 6) the in-order
+  // vmcnt makes those loads wait for the early gathers too (Q6 -6 %,
+  // profiles/r5_dofmap_pipeline.md)
+  constexpr bool EARLY = kDofEarly && GPREF;
   // GLDS: the prefetched stored G of the wave's cells moves as 16-byte
   // chunks (each cell's G block is contiguous) and is redistributed to the
   // quadrature lanes through LDS at the F stage: 12 instead of 30 load
@@ -279,8 +295,9 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
         const int e = (lane + 64 * m) * GW;  // first value of this lane's chunk
         if (e < GE) {
           const int s = e / (6 * NQ3);
-          Gv[m] = *reinterpret_cast<const GV*>(A.G + static_cast<int64_t>(cell_at(j, s)) * 6 * NQ3 +
-                                               (e - s * 6 * NQ3));
+          const GV* gp = reinterpret_cast<const GV*>(A.G + static_cast<int64_t>(cell_at(j, s)) * 6 * NQ3 +
+                                                     (e - s * 6 * NQ3));
+          Gv[m] = kDofGnt ? __builtin_nontemporal_load(gp) : *gp;
         }
       }
     } else if constexpr (GPREF) {
@@ -368,6 +385,15 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
       }
     }
     dof_wave_sync();
+    // early advance: the next cell's gathers into the registers just consumed,
+    // the dofs of the cell after it into dc (the scatter targets are in dsc)
+    if constexpr (EARLY) {
+      const int cn = cell_of(j + 1), cnn = cell_of(j + 2);
+      gather(dn, vn, j + 1, cn, gc);
+      load_dofs(j + 2, dc);
+      load_verts(cnn, vc);
+      cell_cur = cn;
+    }
 
     // ---- interpolation to the quadrature points: z (nodal lanes), y (mixed), x (quad)
     T U[LPL][NQ];
@@ -501,6 +527,7 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
           if (e < GE) *reinterpret_cast<GV*>(&s_G[wv][e]) = Gv[m];
         }
         dof_wave_sync();
+        if constexpr (EARLY) load_G(j + 1, cell_of(j + 1));
       }
 #pragma unroll
       for (int rp = 0; rp < LPL; ++rp) {
@@ -529,6 +556,7 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
           Cb[(qx * NQ + a) * NQP + b] = kap * (Gd[2] * gx + Gd[4] * gy + Gd[5] * gz);
         }
       }
+      if constexpr (EARLY && GPREF && !GLDS) load_G(j + 1, cell_of(j + 1));
     }
     dof_wave_sync();
 
@@ -650,7 +678,7 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
 
     // ---- advance the pipeline: the next cell's gathers and G, the dofs of
     // the one after (issued before this cell's atomics, which need no wait)
-    {
+    if constexpr (!EARLY) {
       dof_wave_sync();  // the id ring entry of j + 1 / j + 2 is visible
       const int cn = cell_of(j + 1), cnn = cell_of(j + 2);
       gather(dn, vn, j + 1, cn, gc);
