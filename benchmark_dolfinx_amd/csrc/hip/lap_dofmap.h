@@ -548,6 +548,8 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
               Gd[k] = s_G[wv][(slot_on ? slot : 0) * 6 * NQ3 + k * NQ3 + qx * NQ2 + sl + 64 * rp];
             else if constexpr (GPREF)
               Gd[k] = Gr[rp][k * NQ + qx];
+            else if constexpr (kDofGnt)
+              Gd[k] = __builtin_nontemporal_load(&A.G[cell * 6 * NQ3 + k * NQ3 + qx * NQ2 + sl + 64 * rp]);
             else
               Gd[k] = A.G[cell * 6 * NQ3 + k * NQ3 + qx * NQ2 + sl + 64 * rp];
           }
