@@ -95,6 +95,10 @@ struct DofArgs {
   const double* scal;
   int beta_num, beta_den, xa_num, xa_den;  // -1: beta = 0 / no x update
   double* partials;                        // CG: p.Ap per block
+  // native CG runtime: the other y buffer of its ping-pong (consumed by the
+  // last update pass), zeroed by this launch for the next operator; null: none
+  T* yz;
+  int64_t nz;
 };
 
 // wave-local LDS exchange (the lanes of one wave run in lockstep)
@@ -710,7 +714,19 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     iter(j, dA, dB, vA, vB);
     if (j + 1 < nit) iter(j + 1, dB, dA, vB, vA);
   }
+  // zero this block's slice of the other y buffer (after the cell loop, so
+  // the stores never sit in front of a wait for the pipeline's loads)
   if constexpr (MODE == kDofCG) {
+    if (A.yz) {
+      constexpr int W = 16 / sizeof(T);
+      typedef T ZV __attribute__((ext_vector_type(16 / sizeof(T))));
+      const int64_t nv = A.nz / W, per = (nv + nblk - 1) / nblk;
+      const int64_t v0 = static_cast<int64_t>(ob) * per, v1 = v0 + per < nv ? v0 + per : nv;
+      for (int64_t v = v0 + tid; v < v1; v += S::NT)
+        __builtin_nontemporal_store(ZV(0), reinterpret_cast<ZV*>(A.yz + v * W));
+      if (ob == 0)
+        for (int64_t i = nv * W + tid; i < A.nz; i += S::NT) A.yz[i] = T(0);
+    }
     const double t = block_sum(pap, s_red);
     if (tid == 0) A.partials[bid] = t;
   }
@@ -767,7 +783,9 @@ static __global__ void __launch_bounds__(256)
 constexpr int kDofUpdU = 4;
 
 // CG update of the dofmap path: alpha = s[rn] / s[pap]; r -= alpha y over
-// every local dof, r.r over the owned ones, y = 0 for the next operator.
+// every local dof, r.r over the owned ones, y = 0 for the next operator
+// (ZERO; the native runtime's y ping-pong leaves that to the next operator
+// launch, DofArgs::yz).
 // 16-byte vectors (and W flag bytes); block 0 takes the tail.  Non-temporal
 // r / y loads and stores (a pure stream): update pass Q3 2.29 -> 2.00 ms, Q6
 // 3.07 -> 2.74, +1.5 % / +2-4 % GDoF/s same box (profiles/r4_update_pass_ab.txt).
@@ -776,7 +794,7 @@ constexpr int kDofUpdU = 4;
 // fused_common.hip): with one vector per thread and pass the loop kept a
 // single 16-byte r / y pair in flight per thread and ran 1.56 ms on one box
 // and 2.17 ms on another at Q3 (profiles/r5_dofmap_update.md).
-template <typename T, int U>
+template <typename T, int U, bool ZERO>
 __global__ void __launch_bounds__(256)
     dofmap_cg_update_kernel(int64_t n, const unsigned char* __restrict__ flags, T* __restrict__ r,
                             T* __restrict__ y, const double* __restrict__ scal, int rn_slot,
@@ -808,7 +826,7 @@ __global__ void __launch_bounds__(256)
       if (v >= nv) break;
       const V rn = vr[u] - alpha * vy[u];
       __builtin_nontemporal_store(rn, reinterpret_cast<V*>(r + v * W));
-      __builtin_nontemporal_store(V(0), reinterpret_cast<V*>(y + v * W));
+      if constexpr (ZERO) __builtin_nontemporal_store(V(0), reinterpret_cast<V*>(y + v * W));
 #pragma unroll
       for (int w = 0; w < W; ++w)
         if (fl[u][w] & 2u) acc += static_cast<double>(rn[w]) * static_cast<double>(rn[w]);
@@ -818,7 +836,7 @@ __global__ void __launch_bounds__(256)
     for (int64_t i = nv * W + threadIdx.x; i < n; i += blockDim.x) {
       const T rn = r[i] - alpha * y[i];
       r[i] = rn;
-      y[i] = T(0);
+      if constexpr (ZERO) y[i] = T(0);
       if (flags[i] & 2u) acc += static_cast<double>(rn) * static_cast<double>(rn);
     }
   }
@@ -886,15 +904,33 @@ int launch_dofmap_geometry(int ncells, const int* cverts, const T* coords, const
 // apply: mode 0 = action (u -> y += A u), 1 = CG operator (u = r); returns the
 // number of p.Ap partials written at partials (CG) in *nblocks.
 #define BDX_DOFMAP_API(T, SUF)                                                                    \
+  extern "C" int bdx_dofmap_apply_yz_##SUF(                                                       \
+      int, int, int, int, const T*, const int*, int, int64_t, const int*, const int*, const T*,   \
+      const unsigned char*, const T*, double, const T*, const T*, const T*, T*, T*, T*, T*,       \
+      const double*, int, int, int, int, double*, int*, hipStream_t);                             \
+  extern "C" int bdx_dofmap_cg_update_z_##SUF(int64_t, const unsigned char*, T*, T*,              \
+                                              const double*, int, int, double*, int*, int,        \
+                                              hipStream_t);                                       \
   extern "C" int bdx_dofmap_apply_##SUF(                                                          \
       int P, int nq, int geom, int mode, const T* tab, const int* cells, int ncl, int64_t nvec,   \
       const int* cdofs, const int* cverts, const T* coords, const unsigned char* flags,           \
       const T* G, double kappa, const T* kc, const T* u, const T* pold, T* pnew, T* x, T* y,      \
       const double* scal, int beta_num, int beta_den, int xa_num, int xa_den, double* partials,   \
       int* nblocks, hipStream_t st) {                                                             \
+    return bdx_dofmap_apply_yz_##SUF(P, nq, geom, mode, tab, cells, ncl, nvec, cdofs, cverts,     \
+                                     coords, flags, G, kappa, kc, u, pold, pnew, x, y, nullptr,   \
+                                     scal, beta_num, beta_den, xa_num, xa_den, partials, nblocks, \
+                                     st);                                                         \
+  }                                                                                               \
+  extern "C" int bdx_dofmap_apply_yz_##SUF(                                                       \
+      int P, int nq, int geom, int mode, const T* tab, const int* cells, int ncl, int64_t nvec,   \
+      const int* cdofs, const int* cverts, const T* coords, const unsigned char* flags,           \
+      const T* G, double kappa, const T* kc, const T* u, const T* pold, T* pnew, T* x, T* y,      \
+      T* yz, const double* scal, int beta_num, int beta_den, int xa_num, int xa_den,              \
+      double* partials, int* nblocks, hipStream_t st) {                                           \
     DofArgs<T> a{cells, ncl, 0, nvec, cdofs, cverts, coords, flags, G, tab,                       \
                  static_cast<T>(kappa), kc, u, pold, pnew, x, y, scal, beta_num, beta_den,        \
-                 xa_num, xa_den, partials};                                                       \
+                 xa_num, xa_den, partials, yz, yz ? nvec : 0};                                    \
     if (nvec * static_cast<int64_t>(sizeof(T)) >= 0xfffffff0LL)                                   \
       return static_cast<int>(hipErrorInvalidValue);                                              \
     switch (P * 16 + nq) {                                                                        \
@@ -928,11 +964,22 @@ int launch_dofmap_geometry(int ncells, const int* cverts, const T* coords, const
   extern "C" int bdx_dofmap_cg_update_##SUF(int64_t n, const unsigned char* flags, T* r, T* y,    \
                                             const double* scal, int rn_slot, int pap_slot,        \
                                             double* partials, int* nblocks, hipStream_t st) {     \
+    return bdx_dofmap_cg_update_z_##SUF(n, flags, r, y, scal, rn_slot, pap_slot, partials,        \
+                                        nblocks, 1, st);                                          \
+  }                                                                                               \
+  extern "C" int bdx_dofmap_cg_update_z_##SUF(int64_t n, const unsigned char* flags, T* r, T* y,  \
+                                              const double* scal, int rn_slot, int pap_slot,      \
+                                              double* partials, int* nblocks, int zero_y,         \
+                                              hipStream_t st) {                                   \
     const int64_t want = (n / (16 / static_cast<int64_t>(sizeof(T))) + 256 * kDofUpdU - 1) /      \
                          (256 * kDofUpdU);                                                        \
     const int g = static_cast<int>(want < kDofMaxBlocks ? (want > 0 ? want : 1) : kDofMaxBlocks); \
-    dofmap_cg_update_kernel<T, kDofUpdU><<<g, 256, 0, st>>>(n, flags, r, y, scal, rn_slot,        \
-                                                            pap_slot, partials);                  \
+    if (zero_y)                                                                                   \
+      dofmap_cg_update_kernel<T, kDofUpdU, true>                                                  \
+          <<<g, 256, 0, st>>>(n, flags, r, y, scal, rn_slot, pap_slot, partials);                 \
+    else                                                                                          \
+      dofmap_cg_update_kernel<T, kDofUpdU, false>                                                 \
+          <<<g, 256, 0, st>>>(n, flags, r, y, scal, rn_slot, pap_slot, partials);                 \
     *nblocks = g;                                                                                 \
     return static_cast<int>(hipGetLastError());                                                   \
   }                                                                                               \

@@ -126,6 +126,13 @@ BDX_DECL_F5(float, f32)
       const double*, int, int, int, int, double*, int*, hipStream_t);                          \
   extern "C" int bdx_dofmap_cg_update_##SUF(int64_t, const unsigned char*, T*, T*,              \
                                             const double*, int, int, double*, int*, hipStream_t); \
+  extern "C" int bdx_dofmap_apply_yz_##SUF(                                                   \
+      int, int, int, int, const T*, const int*, int, int64_t, const int*, const int*, const T*, \
+      const unsigned char*, const T*, double, const T*, const T*, const T*, T*, T*, T*, T*,    \
+      const double*, int, int, int, int, double*, int*, hipStream_t);                          \
+  extern "C" int bdx_dofmap_cg_update_z_##SUF(int64_t, const unsigned char*, T*, T*,            \
+                                              const double*, int, int, double*, int*, int,      \
+                                              hipStream_t);                                     \
   extern "C" int bdx_dofmap_xflush_##SUF(int64_t, T*, const T*, const double*, int, int,        \
                                          hipStream_t);
 BDX_DECL_DOF(double, f64)
@@ -1214,33 +1221,49 @@ struct DofCGRuntime final : LoopBase {
   const unsigned char* flags = nullptr;
   T *x, *r, *pa, *pb, *y;
   double *scal, *partials, *upart;
+  // y ping-pong: iteration k's operator adds into yk(k) and zeroes yk(k + 1)
+  // (consumed by the update pass of iteration k - 1), so the update pass
+  // streams r, y and r back and no longer writes y = 0 (one vector stream
+  // less per iteration; the zero stores ride in the operator's tail).  y2 is
+  // the runtime's own second buffer; y (the caller's) is yk of even k.
+  T* y2 = nullptr;
+  T* yk(long k) const { return (k % 2 == 0) ? y : y2; }
+
+  ~DofCGRuntime() override {
+    if (y2) (void)hipFree(y2);
+  }
 
   void* halo_vector() override { return r; }
 
-  int run(const int* cells, int ncl, double* part, long k, bool first, bool xlag,
+  // zero: this launch also zeroes yk(k + 1)
+  int run(const int* cells, int ncl, double* part, long k, bool first, bool xlag, bool zero,
           hipStream_t s) {
     if (ncl <= 0) return 0;
     const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
     T* pold = (k % 2 == 0) ? pa : pb;
     T* pnew = (k % 2 == 0) ? pb : pa;
+    T* const yz = zero ? yk(k + 1) : nullptr;
     int nb = 0;
     int rc;
     if constexpr (sizeof(T) == 8)
-      rc = bdx_dofmap_apply_f64(cfg.P, cfg.nq, cfg.geom, 1, tab, cells, ncl, cfg.nvec, cdofs,
-                                cverts, coords, flags, G, cfg.kappa, kc, r, pold, pnew, x, y, scal,
-                                first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
-                                xlag ? kPAP : -1, part, &nb, s);
+      rc = bdx_dofmap_apply_yz_f64(cfg.P, cfg.nq, cfg.geom, 1, tab, cells, ncl, cfg.nvec, cdofs,
+                                   cverts, coords, flags, G, cfg.kappa, kc, r, pold, pnew, x,
+                                   yk(k), yz, scal, first ? -1 : cur, first ? -1 : nxt,
+                                   xlag ? nxt : -1, xlag ? kPAP : -1, part, &nb, s);
     else
-      rc = bdx_dofmap_apply_f32(cfg.P, cfg.nq, cfg.geom, 1, tab, cells, ncl, cfg.nvec, cdofs,
-                                cverts, coords, flags, G, cfg.kappa, kc, r, pold, pnew, x, y, scal,
-                                first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
-                                xlag ? kPAP : -1, part, &nb, s);
+      rc = bdx_dofmap_apply_yz_f32(cfg.P, cfg.nq, cfg.geom, 1, tab, cells, ncl, cfg.nvec, cdofs,
+                                   cverts, coords, flags, G, cfg.kappa, kc, r, pold, pnew, x,
+                                   yk(k), yz, scal, first ? -1 : cur, first ? -1 : nxt,
+                                   xlag ? nxt : -1, xlag ? kPAP : -1, part, &nb, s);
     return rc;
   }
 
   int step(long k, bool first, bool xlag, int /*xm*/) override {
     const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
     double* const part_b = partials + cfg.nb_inner;
+    T* const yc = yk(k);
+    // the interior launch zeroes yk(k + 1); the boundary one when there is none
+    const bool z_in = cfg.n_inner > 0, z_out = !z_in;
     int rc;
     mark(kMStart, st);
     if (split) {
@@ -1254,31 +1277,31 @@ struct DofCGRuntime final : LoopBase {
       mark(kMFwdBeg, cs);
       if ((rc = halo_forward(r, cs))) return rc;
       mark(kMFwdEnd, cs);
-      if ((rc = run(outer, cfg.n_outer, part_b, k, first, xlag, cs))) return rc;
+      if ((rc = run(outer, cfg.n_outer, part_b, k, first, xlag, z_out, cs))) return rc;
       mark(kMBnd, cs);
       mark(kMRevBeg, cs);
-      if ((rc = halo_reverse_send(y, cs))) return rc;
+      if ((rc = halo_reverse_send(yc, cs))) return rc;
       BDX_CHECK(hipEventRecord(ev_rev, cs));
       mark(kMRevEnd, cs);
       if ((rc = interior([&](hipStream_t s) {
-             const int r2 = run(inner, cfg.n_inner, partials, k, first, xlag, s);
+             const int r2 = run(inner, cfg.n_inner, partials, k, first, xlag, z_in, s);
              mark(kMOpA, s);
              return r2;
            })))
         return rc;
       BDX_CHECK(hipStreamWaitEvent(st, ev_rev, 0));
-      if ((rc = halo_reverse_add(y, st))) return rc;
+      if ((rc = halo_reverse_add(yc, st))) return rc;
       mark(kMJoin, st);
     } else {
       mark(kMFwdBeg, st);
       if (halo && (rc = halo_forward(r, st))) return rc;
       mark(kMFwdEnd, st);
-      if ((rc = run(inner, cfg.n_inner, partials, k, first, xlag, st))) return rc;
+      if ((rc = run(inner, cfg.n_inner, partials, k, first, xlag, z_in, st))) return rc;
       mark(kMOpA, st);
-      if ((rc = run(outer, cfg.n_outer, part_b, k, first, xlag, st))) return rc;
+      if ((rc = run(outer, cfg.n_outer, part_b, k, first, xlag, z_out, st))) return rc;
       mark(kMBnd, st);
       mark(kMRevBeg, st);
-      if (halo && ((rc = halo_reverse_send(y, st)) || (rc = halo_reverse_add(y, st)))) return rc;
+      if (halo && ((rc = halo_reverse_send(yc, st)) || (rc = halo_reverse_add(yc, st)))) return rc;
       mark(kMRevEnd, st);
       mark(kMJoin, st);
     }
@@ -1288,9 +1311,9 @@ struct DofCGRuntime final : LoopBase {
     mark(kMPap, st);
     int nu = 0;
     if constexpr (sizeof(T) == 8)
-      rc = bdx_dofmap_cg_update_f64(cfg.nvec, flags, r, y, scal, cur, kPAP, upart, &nu, st);
+      rc = bdx_dofmap_cg_update_z_f64(cfg.nvec, flags, r, yc, scal, cur, kPAP, upart, &nu, 0, st);
     else
-      rc = bdx_dofmap_cg_update_f32(cfg.nvec, flags, r, y, scal, cur, kPAP, upart, &nu, st);
+      rc = bdx_dofmap_cg_update_z_f32(cfg.nvec, flags, r, yc, scal, cur, kPAP, upart, &nu, 0, st);
     if (rc || (rc = bdx_reduce_partials(upart, nu, scal, nxt, st))) return rc;
     mark(kMUpd, st);
     if (nranks > 1 && (rc = tr->allreduce_sum(scal + nxt, 1, st))) return rc;
@@ -1456,6 +1479,11 @@ LoopBase* create_dofmap(const int64_t* latd, const int* iparams, int64_t nvec, d
   rt->G = static_cast<const T*>(ptrs[i++]);
   rt->kc = static_cast<const T*>(ptrs[i++]);
   if (!rt->tab || !rt->cdofs || !rt->flags || (c.geom == kGeomStored && !rt->G)) return nullptr;
+  if (hipMalloc(&rt->y2, static_cast<size_t>(nvec) * sizeof(T)) != hipSuccess ||
+      hipMemset(rt->y2, 0, static_cast<size_t>(nvec) * sizeof(T)) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
   rt->wlatd = c.latd;
   if (rt->init_common(st, hptrs, halo_sizes, face_cnt, ghost_cnt, transport, nranks, rank,
                       group_id))
