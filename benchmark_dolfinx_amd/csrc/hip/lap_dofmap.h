@@ -52,8 +52,12 @@ enum { kDofAction = 0, kDofCG = 1 };
 // element stage has consumed the current ones, and the next cell's stored G
 // as soon as the F stage has moved the current G to LDS, so both are in
 // flight for a whole iteration instead of from the end of one to the start /
-// middle of the next (stored-G instances).  kDofGnt streams G non-temporally (66.6 GB per apply
-// at Q3, read once: kept out of the caches that the gathers reuse).
+// middle of the next (instances that prefetch G).  kDofGnt streams G
+// non-temporally (66.6 GB per apply at Q3, read once: kept out of the caches
+// that the gathers reuse).  A direct-to-LDS form of the G staging
+// (global_load_lds_dwordx4) compiles to a vmcnt(0) before the next read of
+// any LDS array (the waitcnt pass cannot separate s_G from s_buf), which
+// would expose the G latency at once: not used.
 constexpr bool kDofEarly = true;
 constexpr bool kDofGnt = true;
 typedef unsigned bdx_u32x2 __attribute__((ext_vector_type(2)));
