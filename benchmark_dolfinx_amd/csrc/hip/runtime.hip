@@ -544,11 +544,11 @@ struct LoopBase {
   long it = 0;
   // Lagged x update: `pend` terms alpha_j p_j are not yet in x (0, 1 or 2).
   // One-term kernels fold alpha_prev p_old into x at every iteration (pend
-  // stays 1).  fused5 pairs them (xpair): an iteration with one term pending
-  // only saves alpha_prev (kXSave), the next folds both, reading p_prev2 from
-  // the p buffer it is about to overwrite (kXPair) -- x is read and written
-  // every other iteration, for one extra p read: 5.5 instead of 6 operator
-  // streams per iteration.
+  // stays 1).  fused5 can pair them (xpair, the FP32 default): an iteration
+  // with one term pending only saves alpha_prev (kXSave), the next folds
+  // both, reading p_prev2 from the p buffer it is about to overwrite (kXPair)
+  // -- x is read and written every other iteration, for one extra p read:
+  // 5.5 instead of 6 operator streams per iteration, but unevenly spread.
   int pend = 0;
   bool xpair = false;
   bool use_graph = true, graph_ok[4] = {false, false, false, false};
@@ -1364,11 +1364,16 @@ LoopBase* create(const int64_t* latd, const int64_t* own, const int* iparams, do
   c.wts.assign(wts, wts + c.nq);
   c.qpts.assign(qpts, qpts + c.nq);
   rt->apply = apply_fn<T>(c.version, c.P);
-  // paired lagged x update (fused5 only; BDX_XPAIR=0 keeps one term per
-  // iteration, for A/B runs)
+  // paired lagged x update (fused5 only): FP32 by default; FP64 folds one
+  // term per iteration, which spreads the x stream evenly over the
+  // iterations -- the paired form's every other iteration carries x, x and
+  // p_prev2 at once and the FP64 operator does not hide that burst: Q6 FP64
+  // +2.3-3.7 %, Q3 +1.2-2.1 %, Q6 FP32 -0.1-0.7 % with one term, same box
+  // (profiles/r5_xpair_ab.md).  BDX_XPAIR=0 / 1 forces either form.
   {
     const char* e = std::getenv("BDX_XPAIR");
-    rt->xpair = c.version == 5 && !(e && e[0] == '0');
+    const bool dflt = sizeof(T) == 4;
+    rt->xpair = c.version == 5 && (e && e[0] ? e[0] != '0' : dflt);
   }
   if (!rt->apply || !tabs) return nullptr;
   if (c.version == 5) {
