@@ -60,7 +60,7 @@ __device__ __forceinline__ double dpp_row_ror8(double v) {
 // entry points' mode word, set by runtime.hip): one term per iteration, save
 // alpha_prev only, or fold two terms; the saved alpha's slot of the CG scalars.
 enum { kXSingle = 0, kXSave = 1, kXPair = 2 };
-constexpr int kScalXSave = 3;
+constexpr int kScalXSave = 3;  // and kScalXSave + 1 (alternate iterations)
 
 // Debug builds (BDX_DEBUG=1: `python -m benchmark_dolfinx_amd.ops.build
 // --variant debug=-DBDX_DEBUG=1`, loaded with BDX_HIP_LIB) turn on

@@ -201,7 +201,8 @@ __global__ void __launch_bounds__(kBlock)
     flush_export_kernel(int64_t L0, int64_t L1, int64_t L2, int64_t ld, int tsy, int tsz,
                         int tntz, int ngz, T* __restrict__ a, T* __restrict__ t,
                         const T* __restrict__ p1, const T* __restrict__ p2,
-                        const double* __restrict__ scal, int num1, int den1, int num2, int den2) {
+                        const double* __restrict__ scal, int num1, int den1, int num2, int den2,
+                        int p2mask) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fe_lds[];
   T* const sv = reinterpret_cast<T*>(fe_lds);  // [tsy][kFeTiles * tsz]
   const T a1 = static_cast<T>(den1 < 0 ? scal[num1] : scal[num1] / scal[den1]);
@@ -222,7 +223,9 @@ __global__ void __launch_bounds__(kBlock)
     const int64_t off = (cbase + static_cast<int64_t>(tl) * L0) * C + e;
     V vt = __builtin_nontemporal_load(reinterpret_cast<const V*>(t + off));
     vt += a1 * __builtin_nontemporal_load(reinterpret_cast<const V*>(p1 + off));
-    if (p2) vt += a2 * __builtin_nontemporal_load(reinterpret_cast<const V*>(p2 + off));
+    // p2mask: the tile colours ((ty + tz) & 1) with the second term pending
+    if (p2 && ((p2mask >> ((ty + tz0 + tl) & 1)) & 1))
+      vt += a2 * __builtin_nontemporal_load(reinterpret_cast<const V*>(p2 + off));
     __builtin_nontemporal_store(vt, reinterpret_cast<V*>(t + off));
     int ly = e / tsz, lz = e - ly * tsz;
 #pragma unroll
@@ -348,11 +351,11 @@ int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
     return static_cast<int>(hipGetLastError());                               \
   }                                                                           \
   /* tiled x += a1 p1 [+ a2 p2], exported to the lattice layout (p2 may be */ \
-  /* null) */                                                                 \
+  /* null; p2mask: tile colours that take it, 3 = every tile) */              \
   int bdx_flush_export_##SUF(const int64_t* latd_tiled, T* lat, T* tiled,     \
                              const T* p1, const T* p2, const double* scal,    \
                              int num1, int den1, int num2, int den2,          \
-                             hipStream_t st) {                                \
+                             int p2mask, hipStream_t st) {                    \
     const BdxLattice L = BdxLattice::from(latd_tiled);                        \
     if (!L.tsy || (L.tsy * L.tsz * static_cast<int64_t>(sizeof(T))) % 16)    \
       return static_cast<int>(hipErrorInvalidValue);                          \
@@ -366,7 +369,7 @@ int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
     flush_export_kernel<T><<<static_cast<unsigned>(nblk), kBlock, lds, st>>>( \
         L.L[0], L.L[1], L.L[2], L.ld, static_cast<int>(L.tsy),                \
         static_cast<int>(L.tsz), static_cast<int>(L.tntz), ngz, lat, tiled,   \
-        p1, p2, scal, num1, den1, num2, den2);                                \
+        p1, p2, scal, num1, den1, num2, den2, p2mask);                        \
     return static_cast<int>(hipGetLastError());                               \
   }
 

@@ -57,9 +57,11 @@ struct Fused2Args {
   int xa_num, xa_den;            // CG: alpha_prev = scal[num] / scal[den]; num < 0 -> no x update
   // fused5 CG: paired lagged x update (kXSave, kXPair; 0 = one term per
   // iteration).  kXSave: no x update, alpha_prev is stored to
-  // scal[kScalXSave]; kXPair: x += alpha_prev p_old + scal[kScalXSave] p_prev2,
+  // scal[xslot_w]; kXPair: x += alpha_prev p_old + scal[xslot_r] p_prev2,
   // p_prev2 being read from pnew before it is overwritten (runtime.hip).
-  int xmode;
+  // xmode1 >= 0: the x mode of the odd tiles ((ty + tz) odd) of a staggered
+  // pairing, in which the two tile colours pair on alternate iterations.
+  int xmode, xmode1, xslot_w, xslot_r;
   T kappa;
   // tiled vector storage (bdx_lattice.h; tsy = 0: lattice layout): the
   // x-plane stride ps is then tsy * tsz and a node's (y, z) offset is its
@@ -796,6 +798,8 @@ template <typename T>
 inline int make_fused2_args(Fused2Args<T>& a, const int64_t* latd, int nty, int ntz) {
   const BdxLattice L = BdxLattice::from(latd);
   a.xmode = 0;
+  a.xmode1 = -1;
+  a.xslot_w = a.xslot_r = kScalXSave;
   const int64_t P = L.P;
   // 32-bit per-layer offsets: one layer of the vector must be < 2^31 elements
   if ((P + 1) * L.L[1] * L.ld >= (int64_t(1) << 31)) return static_cast<int>(hipErrorInvalidValue);
@@ -928,7 +932,7 @@ inline int fused_set_segments(Fused2Args<T>& a, int nseg) {
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     if (a.tsy) return static_cast<int>(hipErrorInvalidValue); /* lattice layout only */ \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
-    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, (mode >> 8) & 0xff))); \
     mode &= 0xff;                                                                  \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \

@@ -1324,7 +1324,7 @@ int fused3_resident(int affine) {
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
-    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, (mode >> 8) & 0xff))); \
     mode &= 0xff;                                                                  \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \

@@ -221,15 +221,20 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
   // alpha_prev (kXSave), or two terms: + alpha_prev2 p_prev2 read from pnew
   // before this iteration overwrites it (kXPair; saves the x read / write of
   // every other iteration, runtime.hip)
+  // staggered pairing: the odd tiles run xmode1 (they pair when the even
+  // ones save, so every iteration carries half of the x stream)
   T beta = T(0), xalpha = T(0), xalpha2 = T(0);
-  const bool xupd = MODE == kFusedCG && A.xa_num >= 0 && A.xmode != kXSave;
-  const bool xpair = xupd && A.xmode == kXPair;
+  const int xm = (A.xmode1 >= 0 && ((ty + tz) & 1)) ? A.xmode1 : A.xmode;
+  const bool xupd = MODE == kFusedCG && A.xa_num >= 0 && xm != kXSave;
+  const bool xpair = xupd && xm == kXPair;
   if constexpr (MODE == kFusedCG) {
     if (A.beta_num >= 0) beta = static_cast<T>(A.scal[A.beta_num] / A.scal[A.beta_den]);
     if (xupd) xalpha = static_cast<T>(A.scal[A.xa_num] / A.scal[A.xa_den]);
-    if (xpair) xalpha2 = static_cast<T>(A.scal[kScalXSave]);
-    if (A.xmode == kXSave && A.xa_num >= 0 && blockIdx.x == 0 && threadIdx.x == 0)
-      const_cast<double*>(A.scal)[kScalXSave] = A.scal[A.xa_num] / A.scal[A.xa_den];
+    if (xpair) xalpha2 = static_cast<T>(A.scal[A.xslot_r]);
+    // every saving block writes the same value (any block of the saving
+    // colour may be the first of a launch rectangle)
+    if (xm == kXSave && A.xa_num >= 0 && threadIdx.x == 0 && (A.xmode1 >= 0 || blockIdx.x == 0))
+      const_cast<double*>(A.scal)[A.xslot_w] = A.scal[A.xa_num] / A.scal[A.xa_den];
   }
   double pap = 0.0;
 
@@ -1016,8 +1021,11 @@ int launch_fused5(int affine_ok, const Fused2Args<T>& a, const T* tabd, hipStrea
     Fused2Args<T> a;                                                               \
     BDX_CHECK(static_cast<hipError_t>(make_fused2_args(a, latd, nty, ntz)));  \
     BDX_CHECK(static_cast<hipError_t>(fused_set_rect(a, rect)));       \
-    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, mode >> 8)));    \
+    BDX_CHECK(static_cast<hipError_t>(fused_set_segments(a, (mode >> 8) & 0xff))); \
     a.xmode = (mode >> 4) & 3;                                                     \
+    a.xmode1 = ((mode >> 6) & 3) - 1;                                              \
+    a.xslot_w = kScalXSave + ((mode >> 16) & 1);                                   \
+    a.xslot_r = kScalXSave + ((mode >> 17) & 1);                                   \
     mode &= 0xf;                                                                   \
     a.u = u;                                                                       \
     a.pold = pold;                                                                 \

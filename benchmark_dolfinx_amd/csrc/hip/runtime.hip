@@ -83,9 +83,9 @@ int bdx_box_copy_lat_f32(int, float*, const int64_t*, const int64_t*, int, int64
 int bdx_layout_convert_f64(int, const int64_t*, double*, double*, hipStream_t);
 int bdx_layout_convert_f32(int, const int64_t*, float*, float*, hipStream_t);
 int bdx_flush_export_f64(const int64_t*, double*, double*, const double*, const double*,
-                         const double*, int, int, int, int, hipStream_t);
+                         const double*, int, int, int, int, int, hipStream_t);
 int bdx_flush_export_f32(const int64_t*, float*, float*, const float*, const float*,
-                         const double*, int, int, int, int, hipStream_t);
+                         const double*, int, int, int, int, int, hipStream_t);
 int bdx_cg_update_tiled_f64(const int64_t*, const int64_t*, double*, const double*, const double*,
                             const double*, const double*, int, int, double*, int, int, int,
                             double*, hipStream_t);
@@ -544,13 +544,21 @@ struct LoopBase {
   long it = 0;
   // Lagged x update: `pend` terms alpha_j p_j are not yet in x (0, 1 or 2).
   // One-term kernels fold alpha_prev p_old into x at every iteration (pend
-  // stays 1).  fused5 can pair them (xpair, the FP32 default): an iteration
+  // stays 1).  fused5 pairs them (xpair): an iteration
   // with one term pending only saves alpha_prev (kXSave), the next folds
   // both, reading p_prev2 from the p buffer it is about to overwrite (kXPair)
   // -- x is read and written every other iteration, for one extra p read:
   // 5.5 instead of 6 operator streams per iteration, but unevenly spread.
   int pend = 0;
   bool xpair = false;
+  // Staggered pairing (xpair on tiled storage, BDX_XSTAGGER): the odd tiles
+  // ((ty + tz) odd) run the save / pair cycle one iteration out of phase
+  // with their own pending count pend1, so every iteration carries half of
+  // the x stream instead of all of it every other iteration.  The saved
+  // alpha alternates between two scalar slots (kScalXSave + iteration parity).
+  bool stagger = false;
+  int pend1 = 0;
+  int cur_m1 = kXSingle;  // the odd tiles' mode of the iteration being launched
   bool use_graph = true, graph_ok[4] = {false, false, false, false};
   hipGraphExec_t graph[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_batch[2] = {nullptr, nullptr};  // in-flight bound (iterate_on_stream)
@@ -734,7 +742,22 @@ struct LoopBase {
     if (pend == 0 || !xpair) return kXSingle;
     return pend == 1 ? kXSave : kXPair;
   }
-  void advance_pend(int xm) { pend = (pend == 0 || xm == kXPair) ? 1 : (xm == kXSave ? 2 : 1); }
+  // the odd tiles' mode for an even-tile mode m0 (staggered pairing)
+  int next_xmode1(int m0) const {
+    if (!stagger) return m0;
+    if (m0 == kXSave) return pend1 == 2 ? kXPair : kXSingle;
+    if (m0 == kXPair) return kXSave;
+    return kXSingle;
+  }
+  static int advanced(int p, int xm) { return (p == 0 || xm == kXPair) ? 1 : (xm == kXSave ? 2 : 1); }
+  void advance_pend(int xm, int xm1) {
+    pend = advanced(pend, xm);
+    pend1 = stagger ? advanced(pend1, xm1) : pend;
+  }
+  // the periodic regime, in which one graph per (parity, even-tile mode) holds
+  static bool periodic(int m0, int m1) {
+    return (m0 == kXSave && m1 == kXPair) || (m0 == kXPair && m1 == kXSave);
+  }
 
   // Capture the steady-state iteration of a parity and x mode (it > 0,
   // lagged x update pending); graph index = parity + 2 * (xm == kXPair).
@@ -809,8 +832,9 @@ struct LoopBase {
         const bool first = (it == 0);
         const int par = static_cast<int>(it % 2);
         const int xm = next_xmode();
+        cur_m1 = next_xmode1(xm);
         const int gi = par + 2 * (xm == kXPair);
-        const bool steady = !first && pend > 0 && !prof;
+        const bool steady = !first && pend > 0 && !prof && (!stagger || periodic(xm, cur_m1));
         if (steady && use_graph && tr->capturable() && !graph_ok[gi]) {
           graph_ok[gi] = capture(par, xm);
           if (!graph_ok[gi]) use_graph = false;  // fall back to eager launches
@@ -821,7 +845,7 @@ struct LoopBase {
           const int rc = step(it, first, pend > 0, xm);
           if (rc) return rc;
         }
-        advance_pend(xm);
+        advance_pend(xm, cur_m1);
         ++it;
         if (step_ms) BDX_CHECK(hipEventRecord(tev[i + 1], st));
       }
@@ -853,9 +877,10 @@ struct LoopBase {
     for (long i = 0; i < n && !rc; ++i) {
       const bool first = (it == 0);
       const int xm = next_xmode();
+      cur_m1 = next_xmode1(xm);
       rc = step(it, first, pend > 0, xm);
       if (rc) break;
-      advance_pend(xm);
+      advance_pend(xm, cur_m1);
       ++it;
       if ((rc = static_cast<int>(hipEventRecord(ev_out, st)))) break;
       if ((rc = tr->wait(ev_out))) break;
@@ -993,7 +1018,13 @@ struct CGRuntime final : LoopBase {
     const int cur = (k % 2 == 0) ? kRR0 : kRR1, nxt = cur == kRR0 ? kRR1 : kRR0;
     T* pold = (k % 2 == 0) ? wpa : wpb;
     T* pnew = (k % 2 == 0) ? wpb : wpa;
-    return apply(1 | (xm << 4) | (cfg.nseg << 8), cfg.affine, wlatd, cfg.nq, cfg.wts.data(),
+    // mode word: CG | x mode (bits 4-5) | odd-tile x mode + 1 (6-7, 0: not
+    // staggered) | segments (8-15) | saved-alpha slot parity to write (16)
+    // and to read (17)
+    const int m1 = stagger ? cur_m1 + 1 : 0;
+    const int word = 1 | (xm << 4) | (m1 << 6) | (cfg.nseg << 8) | static_cast<int>((k & 1) << 16) |
+                     static_cast<int>(((k + 1) & 1) << 17);
+    return apply(word, cfg.affine, wlatd, cfg.nq, cfg.wts.data(),
                  cfg.qpts.data(), wr, pold, pnew, wx, wy, yb, zb, cb, xv, kc, tabs, cfg.kappa,
                  scal, partials, first ? -1 : cur, first ? -1 : nxt, xlag ? nxt : -1,
                  xlag ? kPAP : -1, cfg.nty, cfg.ntz, rect, s);
@@ -1082,20 +1113,23 @@ struct CGRuntime final : LoopBase {
   // x += alpha_last p_last (and, with two terms pending, the saved
   // alpha_prev p_prev, which is the last iteration's p_old)
   int flush() override {
-    if (pend == 0) return 0;
+    if (pend == 0 && pend1 == 0) return 0;
     const int last = ((it - 1) % 2 == 0) ? kRR0 : kRR1;
     T* plast = ((it - 1) % 2 == 0) ? wpb : wpa;  // p_new of the last iteration
     T* pprev = ((it - 1) % 2 == 0) ? wpa : wpb;  // its p_old
-    const bool two = pend == 2;
-    pend = 0;
+    // two terms pending: alpha_prev was saved by the last iteration
+    const int slot = kScalXSave + static_cast<int>((it - 1) & 1);
+    const bool two = pend == 2, two1 = stagger ? pend1 == 2 : two;
+    pend = pend1 = 0;
     if (is_tiled) {  // fold the terms and export x in one pass
-      const T* p2 = two ? pprev : nullptr;
+      const T* p2 = (two || two1) ? pprev : nullptr;
+      const int mask = (two ? 1 : 0) | (two1 ? 2 : 0);  // tile colours with two terms
       if constexpr (sizeof(T) == 8)
-        return bdx_flush_export_f64(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
-                                    -1, st);
+        return bdx_flush_export_f64(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, slot, -1, mask,
+                                    st);
       else
-        return bdx_flush_export_f32(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, kScalXSave,
-                                    -1, st);
+        return bdx_flush_export_f32(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, slot, -1, mask,
+                                    st);
     }
     auto one = [&](T* p, int num, int den) {
       if constexpr (sizeof(T) == 8)
@@ -1104,7 +1138,7 @@ struct CGRuntime final : LoopBase {
         return bdx_xflush_f32(cfg.latd, cfg.own, x, p, scal, num, den, st);
     };
     int rc = one(plast, last, kPAP);
-    if (!rc && two) rc = one(pprev, kScalXSave, -1);
+    if (!rc && two) rc = one(pprev, slot, -1);
     return rc;
   }
 
@@ -1364,16 +1398,16 @@ LoopBase* create(const int64_t* latd, const int64_t* own, const int* iparams, do
   c.wts.assign(wts, wts + c.nq);
   c.qpts.assign(qpts, qpts + c.nq);
   rt->apply = apply_fn<T>(c.version, c.P);
-  // paired lagged x update (fused5 only): FP32 by default; FP64 folds one
-  // term per iteration, which spreads the x stream evenly over the
-  // iterations -- the paired form's every other iteration carries x, x and
-  // p_prev2 at once and the FP64 operator does not hide that burst: Q6 FP64
-  // +2.3-3.7 %, Q3 +1.2-2.1 %, Q6 FP32 -0.1-0.7 % with one term, same box
-  // (profiles/r5_xpair_ab.md).  BDX_XPAIR=0 / 1 forces either form.
+  // paired lagged x update (fused5 only; BDX_XPAIR=0 folds one term per
+  // iteration).  Paired on every tile at once, every other iteration carries
+  // x, x and p_prev2 and the FP64 operator does not hide that burst (one
+  // term per iteration was 2-4 % faster at Q6 FP64); staggered over the two
+  // tile colours (tiled storage, below) the x stream is spread evenly and
+  // the paired form is the fastest at Q3, Q6 and Q6 FP32
+  // (profiles/r5_xpair_ab.md).
   {
     const char* e = std::getenv("BDX_XPAIR");
-    const bool dflt = sizeof(T) == 4;
-    rt->xpair = c.version == 5 && (e && e[0] ? e[0] != '0' : dflt);
+    rt->xpair = c.version == 5 && !(e && e[0] == '0');
   }
   if (!rt->apply || !tabs) return nullptr;
   if (c.version == 5) {
@@ -1410,6 +1444,12 @@ LoopBase* create(const int64_t* latd, const int64_t* own, const int* iparams, do
     rt->pbt = static_cast<T*>(tptrs[3]);
     rt->yt = static_cast<T*>(tptrs[4]);
     if (!rt->xt || !rt->rt_ || !rt->pat || !rt->pbt || !rt->yt) return nullptr;
+  }
+  // staggered pairing needs the flush's per-tile colours (tiled storage);
+  // BDX_XSTAGGER=0 pairs every tile on the same iterations
+  {
+    const char* e = std::getenv("BDX_XSTAGGER");
+    rt->stagger = rt->xpair && rt->is_tiled && !(e && e[0] == '0');
   }
   rt->wx = rt->is_tiled ? rt->xt : rt->x;
   rt->wr = rt->is_tiled ? rt->rt_ : rt->r;
@@ -1642,7 +1682,7 @@ int bdx_rt_overlap(void* h) {
 int bdx_rt_reset(void* h) {
   return with_rt(h, [](LoopBase* rt) {
     rt->it = 0;
-    rt->pend = 0;
+    rt->pend = rt->pend1 = 0;
     if (auto* f = dynamic_cast<CGRuntime<double>*>(rt)) f->need_import = f->is_tiled;
     if (auto* f = dynamic_cast<CGRuntime<float>*>(rt)) f->need_import = f->is_tiled;
     return 0;

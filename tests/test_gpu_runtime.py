@@ -129,13 +129,16 @@ def test_fused5_operators_keep_their_own_tables_under_graph_replay(monkeypatch, 
 
 @pytest.mark.parametrize("tiled", ["1", "0"])
 @pytest.mark.parametrize("graph", ["0", "1"])
-@pytest.mark.parametrize("xpair", ["1", "0"])
+@pytest.mark.parametrize("xpair", ["1", "0", "1-nostagger"])
 def test_fused5_paired_x_update_any_call_split(monkeypatch, xpair, graph, tiled):
     """fused5's paired lagged x update (kXSave / kXPair in runtime.hip: x is
-    read and written every other iteration) against the host CG, for call
-    splits that leave 1 or 2 terms pending at the flush that ends each call,
-    through iterate, iterate_timed and the profiled iterations."""
-    monkeypatch.setenv("BDX_XPAIR", xpair)
+    read and written every other iteration; on tiled storage staggered, the
+    odd tiles pairing on the even tiles' save iterations) against the host
+    CG, for call splits that leave 1 or 2 terms pending at the flush that
+    ends each call, through iterate, iterate_timed and the profiled
+    iterations."""
+    monkeypatch.setenv("BDX_XPAIR", xpair[0])
+    monkeypatch.setenv("BDX_XSTAGGER", "0" if xpair.endswith("nostagger") else "1")
     monkeypatch.setenv("BDX_GRAPH", graph)
     monkeypatch.setenv("BDX_TILED", tiled)
     nc, P = (4, 5, 6), 3
@@ -163,6 +166,24 @@ def test_fused5_paired_x_update_any_call_split(monkeypatch, xpair, graph, tiled)
         assert rel < 1e-10, (kind, n, total, rel)
     assert cg.it == total
     op.close()
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_fused5_staggered_pairing_multi_rank(monkeypatch, dtype):
+    """Staggered paired x update on 4 threaded ranks (tiled storage, graphs
+    off and on) against one x term per iteration: the same iterate."""
+    nc, P = (5, 9, 10), 3
+    res = {}
+    for mode in ("stagger", "single"):
+        monkeypatch.setenv("BDX_XPAIR", "1" if mode == "stagger" else "0")
+        monkeypatch.setenv("BDX_XSTAGGER", "1")
+        monkeypatch.setenv("BDX_TILED", "1")
+        res[mode] = run_threaded(4, _tiled_job, nc, P, 13, 5, dtype, "random")
+    tol = 1e-11 if dtype == torch.float64 else 2e-4
+    for (a1, a2, t1), (b1, b2, t0) in zip(res["stagger"], res["single"]):
+        assert t1 is True and t0 is True
+        assert abs(a1 - b1) <= tol * abs(b1), (a1, b1)
+        assert abs(a2 - b2) <= tol * abs(b2), (a2, b2)
 
 
 def test_devicecg_solves_twice_with_different_iterates():
