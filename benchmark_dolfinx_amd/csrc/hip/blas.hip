@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(kBlock)
     // p2mask: the tile colours ((ty + tz) & 1) with the second term pending
     if (p2 && ((p2mask >> ((ty + tz0 + tl) & 1)) & 1))
       vt += a2 * __builtin_nontemporal_load(reinterpret_cast<const V*>(p2 + off));
-    __builtin_nontemporal_store(vt, reinterpret_cast<V*>(t + off));
+    if (!(p2mask & 4)) __builtin_nontemporal_store(vt, reinterpret_cast<V*>(t + off));
     int ly = e / tsz, lz = e - ly * tsz;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -351,7 +351,8 @@ int bdx_reduce_partials(const double* partials, int n, double* out, int slot,
     return static_cast<int>(hipGetLastError());                               \
   }                                                                           \
   /* tiled x += a1 p1 [+ a2 p2], exported to the lattice layout (p2 may be */ \
-  /* null; p2mask: tile colours that take it, 3 = every tile) */              \
+  /* null; p2mask bits 0-1: tile colours that take it, bit 2: export only, */ \
+  /* the tiled iterate keeps its lagged terms pending) */                     \
   int bdx_flush_export_##SUF(const int64_t* latd_tiled, T* lat, T* tiled,     \
                              const T* p1, const T* p2, const double* scal,    \
                              int num1, int den1, int num2, int den2,          \

@@ -1120,10 +1120,12 @@ struct CGRuntime final : LoopBase {
     // two terms pending: alpha_prev was saved by the last iteration
     const int slot = kScalXSave + static_cast<int>((it - 1) & 1);
     const bool two = pend == 2, two1 = stagger ? pend1 == 2 : two;
-    pend = pend1 = 0;
-    if (is_tiled) {  // fold the terms and export x in one pass
+    if (is_tiled) {
+      // export x + the pending terms in one pass; the tiled iterate keeps
+      // them pending (the next call continues the lagged chain), which saves
+      // the write-back of the tiled x (one of five streams of the pass)
       const T* p2 = (two || two1) ? pprev : nullptr;
-      const int mask = (two ? 1 : 0) | (two1 ? 2 : 0);  // tile colours with two terms
+      const int mask = (two ? 1 : 0) | (two1 ? 2 : 0) | 4;  // tile colours with two terms
       if constexpr (sizeof(T) == 8)
         return bdx_flush_export_f64(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, slot, -1, mask,
                                     st);
@@ -1131,6 +1133,7 @@ struct CGRuntime final : LoopBase {
         return bdx_flush_export_f32(cfg.latdT, x, wx, plast, p2, scal, last, kPAP, slot, -1, mask,
                                     st);
     }
+    pend = pend1 = 0;
     auto one = [&](T* p, int num, int den) {
       if constexpr (sizeof(T) == 8)
         return bdx_xflush_f64(cfg.latd, cfg.own, x, p, scal, num, den, st);
