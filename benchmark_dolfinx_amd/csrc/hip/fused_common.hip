@@ -31,6 +31,7 @@ int pack_tables(const double* phi0, const double* dphi1, T* out) {
 constexpr int kPartialsCap = 65536, kStage1 = 256;
 constexpr int kUpdGrid = kPartialsCap - kStage1;  // update pass grid cap
 constexpr int kUpdU = 2;  // vectors per thread of the tiled update pass
+constexpr bool kUpdPre = true;  // cg_update_tiled_pre_kernel (interface loads issued up front)
 
 // CG update of the fused2..5 paths: alpha = s[rn] / s[pap];
 //   r -= alpha (y + interface partials);  partial r.r
@@ -247,6 +248,146 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
+// The tiled r update with the tile-interface partials loaded together with
+// the vector's y and r (round 5): in cg_update_tiled_kernel they are loaded
+// inside the branches that need them, after the wave has waited for y and r,
+// so every vector next to a tile interface (a third of them in FP32 at Q6)
+// pays a second memory latency.  Here every load of a pass -- y, r and the
+// YB / ZB / CB terms of each element -- is issued first, as range-checked
+// buffer loads whose offset is out of range (the load returns 0, no memory
+// access) where an element has no such term; the arithmetic follows.  Same
+// sums in the same order as cg_update_tiled_kernel.
+template <typename T, bool ROW, int U>
+__global__ void __launch_bounds__(256)
+    cg_update_tiled_pre_kernel(int64_t L0, int64_t L1, int64_t Lz, int tsy, int tsz, int tntz,
+                               int64_t o0, int64_t o1, int64_t o2, int64_t nvec, T* __restrict__ r,
+                               const T* __restrict__ y, const T* yb, const T* zb, const T* cb,
+                               int nty, int ntz, const double* __restrict__ scal, int rn_slot,
+                               int pap_slot, double* __restrict__ partials) {
+  __shared__ double lds[16];
+  const T alpha = static_cast<T>(scal[rn_slot] / scal[pap_slot]);
+  constexpr int W = 16 / sizeof(T);
+  constexpr int NI = ROW ? W + 2 : 3 * W;  // interface loads per vector
+  typedef T V __attribute__((ext_vector_type(W)));
+  constexpr unsigned kOOB = 0xfffffff0u;
+  auto rsrc = [](const T* ptr, int64_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(ptr), 0,
+                                             static_cast<int>(n * static_cast<int64_t>(sizeof(T))),
+                                             0x00020000);
+  };
+  const auto rs_yb = rsrc(yb, L0 * (nty - 1) * Lz), rs_zb = rsrc(zb, L0 * L1 * (ntz - 1)),
+             rs_cb = rsrc(cb, L0 * (nty - 1) * (ntz - 1));
+  auto ldb = [](__amdgpu_buffer_rsrc_t rs, unsigned off) -> T {
+    if constexpr (sizeof(T) == 8)
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+    else
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+  };
+  auto bo = [](bool on, int64_t e) { return on ? static_cast<unsigned>(e * sizeof(T)) : kOOB; };
+  const int64_t ch = static_cast<int64_t>(tsy) * tsz;
+  const double inv_ch = 1.0 / static_cast<double>(ch);
+  const float inv_l0 = 1.0f / static_cast<float>(L0), inv_tntz = 1.0f / static_cast<float>(tntz);
+  const float inv_tsz = 1.0f / static_cast<float>(tsz);
+  const int l0 = static_cast<int>(L0);
+  double acc = 0.0;
+  for (int64_t vb = static_cast<int64_t>(blockIdx.x) * (256 * U) + threadIdx.x; vb < nvec;
+       vb += static_cast<int64_t>(gridDim.x) * (256 * U)) {
+    V vyu[U], vru[U];
+    T ia[U][NI];
+    int own[U];  // bit w: element w is owned
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = vb + u * 256;
+      own[u] = 0;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) ia[u][i] = T(0);
+      if (v >= nvec) continue;
+      vyu[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(y + v * W));
+      vru[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(r + v * W));
+      const int64_t e0 = v * W;
+      int64_t c = static_cast<int64_t>(static_cast<double>(e0) * inv_ch);  // chunk
+      if (c * ch > e0) --c;
+      if ((c + 1) * ch <= e0) ++c;
+      const int ci = static_cast<int>(c);
+      int blk = static_cast<int>(static_cast<float>(ci) * inv_l0);
+      while (blk * l0 > ci) --blk;
+      while ((blk + 1) * l0 <= ci) ++blk;
+      const int x = ci - blk * l0;
+      int tY = static_cast<int>(static_cast<float>(blk) * inv_tntz);
+      while (tY * tntz > blk) --tY;
+      while ((tY + 1) * tntz <= blk) ++tY;
+      const int tZ = blk - tY * tntz;
+      const int ein = static_cast<int>(e0 - c * ch);
+      int ly = static_cast<int>(static_cast<float>(ein) * inv_tsz);
+      if (ly * tsz > ein) --ly;
+      if ((ly + 1) * tsz <= ein) ++ly;
+      const bool xin = x < o0 && !BDX_OOB(e0 + W - 1, nvec * W, "tiled update");
+      const bool zt = tZ >= 1 && tZ < ntz;
+      if constexpr (ROW) {
+        const int lz0 = ein - ly * tsz;
+        const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz0 = static_cast<int64_t>(tZ) * tsz + lz0;
+        const bool row = xin && gy < o1;
+        const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const bool on = row && gz0 + w < o2;
+          own[u] |= on ? 1 << w : 0;
+          ia[u][w] = ldb(rs_yb, bo(on && yrow >= 0, (x * (nty - 1) + yrow) * Lz + gz0 + w));
+        }
+        const bool z0 = row && gz0 < o2 && lz0 == 0 && zt;
+        ia[u][W] = ldb(rs_zb, bo(z0, (x * L1 + gy) * (ntz - 1) + tZ - 1));
+        ia[u][W + 1] = ldb(rs_cb, bo(z0 && yrow >= 0, (x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1));
+      } else {
+        int lz = ein - ly * tsz - 1;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          if (++lz == tsz) {
+            lz = 0;
+            ++ly;
+          }
+          const int64_t gy = static_cast<int64_t>(tY) * tsy + ly, gz = static_cast<int64_t>(tZ) * tsz + lz;
+          const bool on = xin && gy < o1 && gz < o2;
+          own[u] |= on ? 1 << w : 0;
+          const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
+          const bool zf = on && lz == 0 && zt;
+          ia[u][3 * w] = ldb(rs_yb, bo(on && yrow >= 0, (x * (nty - 1) + yrow) * Lz + gz));
+          ia[u][3 * w + 1] = ldb(rs_zb, bo(zf, (x * L1 + gy) * (ntz - 1) + tZ - 1));
+          ia[u][3 * w + 2] = ldb(rs_cb, bo(zf && yrow >= 0, (x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1));
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = vb + u * 256;
+      if (v >= nvec || !own[u]) continue;
+      V vr = vru[u];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        T t = vyu[u][w];
+        if constexpr (ROW) {  // the order of cg_update_tiled_kernel: y + YB, + ZB, + CB
+          t += ia[u][w];
+          if (w == 0) {
+            t += ia[u][W];
+            t += ia[u][W + 1];
+          }
+        } else {
+          t += ia[u][3 * w];
+          t += ia[u][3 * w + 1];
+          t += ia[u][3 * w + 2];
+        }
+        const T rn = vr[w] - alpha * t;
+        if (own[u] & (1 << w)) {
+          vr[w] = rn;
+          acc += static_cast<double>(rn) * static_cast<double>(rn);
+        }
+      }
+      __builtin_nontemporal_store(vr, reinterpret_cast<V*>(r + v * W));
+    }
+  }
+  const double t = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
 // x += (s[num] / s[den]) p over the owned rows (flush of the lagged x update).
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -343,7 +484,20 @@ BDX_CGI(float, f32)
     const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
     const int64_t want = (nvec + 256 * kUpdU - 1) / (256 * kUpdU);                             \
     const int g = static_cast<int>(want < kUpdGrid ? (want > 0 ? want : 1) : kUpdGrid); \
-    if (sizeof(T) == 4 && L.tsz % 4 == 0)                                                      \
+    /* interface partials prefetched (byte offsets of the buffers fit 31 bits) */          \
+    const bool pre = kUpdPre && L.L[0] * L.L[1] * (ntz > 1 ? ntz - 1 : 1) * 8 < (1LL << 31) &&  \
+                     L.L[0] * (nty > 1 ? nty - 1 : 1) * L.L[2] * 8 < (1LL << 31);              \
+    if (pre && sizeof(T) == 4 && L.tsz % 4 == 0)                                               \
+      cg_update_tiled_pre_kernel<T, true, kUpdU><<<g, 256, 0, st>>>(                           \
+          L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),            \
+          static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,  \
+          scal, rn_slot, pap_slot, partials);                                                  \
+    else if (pre)                                                                              \
+      cg_update_tiled_pre_kernel<T, false, kUpdU><<<g, 256, 0, st>>>(                          \
+          L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),            \
+          static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,  \
+          scal, rn_slot, pap_slot, partials);                                                  \
+    else if (sizeof(T) == 4 && L.tsz % 4 == 0)                                                 \
       cg_update_tiled_kernel<T, true, kUpdU><<<g, 256, 0, st>>>(                               \
           L.L[0], L.L[1], L.L[2], static_cast<int>(L.tsy), static_cast<int>(L.tsz),            \
           static_cast<int>(L.tntz), own[0], own[1], own[2], nvec, r, y, yb, zb, cb, nty, ntz,  \
