@@ -1303,6 +1303,8 @@ struct DofCGRuntime final : LoopBase {
     const bool z_in = cfg.n_inner > 0, z_out = !z_in;
     int rc;
     mark(kMStart, st);
+    if (cfg.n_inner <= 0 && cfg.n_outer <= 0)  // a rank without cells: no launch zeroes it
+      BDX_CHECK(hipMemsetAsync(yk(k + 1), 0, static_cast<size_t>(cfg.nvec) * sizeof(T), st));
     if (split) {
       // cs: forward exchange -> boundary cells -> reverse send of the ghost
       // partials; st: the interior cells (they touch no ghost dof), then the
