@@ -329,10 +329,19 @@ __global__ void __launch_bounds__(256)
         const bool row = xin && gy < o1;
         const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          const bool on = row && gz0 + w < o2;
-          own[u] |= on ? 1 << w : 0;
-          ia[u][w] = ldb(rs_yb, bo(on && yrow >= 0, (x * (nty - 1) + yrow) * Lz + gz0 + w));
+        for (int w = 0; w < W; ++w) own[u] |= (row && gz0 + w < o2) ? 1 << w : 0;
+        // the vector's YB terms: one 16-byte load when they lie in one YB row
+        // (dword-aligned offsets are allowed; the terms of unowned elements
+        // are loaded but not applied), else one load per owned element
+        const bool yneed = row && gz0 < o2 && yrow >= 0;
+        const int64_t ye = (x * (nty - 1) + yrow) * Lz + gz0;
+        if (gz0 + W <= Lz) {
+          const V yv = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs_yb, bo(yneed, ye), 0, 0));
+#pragma unroll
+          for (int w = 0; w < W; ++w) ia[u][w] = yv[w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w) ia[u][w] = ldb(rs_yb, bo(yneed && gz0 + w < o2, ye + w));
         }
         const bool z0 = row && gz0 < o2 && lz0 == 0 && zt;
         ia[u][W] = ldb(rs_zb, bo(z0, (x * L1 + gy) * (ntz - 1) + tZ - 1));
