@@ -18,6 +18,8 @@
 // The math is the reference operator's (tests compare against the C++ CPU
 // operator and the numpy oracle); results differ only by rounding order.
 #pragma once
+#include <type_traits>
+
 #include "lap_fused2.h"
 
 // Unroll of the per-quadrature-point x/F loop.  Parallelepiped instances:
@@ -63,6 +65,9 @@ constexpr bool kF3MfmaBackZ = true;
 // the same three stages in FP32 (v_mfma_f32_16x16x4_f32; bdx_mfma_row maps
 // the FP32 accumulator rows onto the FP64 layout the stages are written for)
 constexpr bool kF3MfmaF32 = true;
+// Dirichlet-free copies of the staging and the gather for the tiles / layers
+// without a boundary node (the split of lap_fused5.h)
+constexpr bool kF3DirSplit = true;
 
 // fused3: fused2's march with direct collocation gradients and wave-local x passes.
 template <typename T, int ND, int NQ, int TY, int TZ, int MODE, int AFF, bool VEC = false>
@@ -169,6 +174,12 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads),
   const int ez = (z0 + DZ <= Lz) ? DZ : Lz - z0;
   const int oy = top_y ? ey : TY * P;
   const int oz = top_z ? ez : TZ * P;
+  // Dirichlet work only where a tile holds a y / z boundary node or a layer
+  // an x boundary plane (workgroup-uniform; see lap_fused5.h)
+  auto in_rng = [](int v, int lo, int n) { return v >= lo && v < lo + n; };
+  const bool tile_bc = in_rng(A.bcy_lo, y0, ey) || in_rng(A.bcy_hi, y0, ey) ||
+                       in_rng(A.bcz_lo, z0, ez) || in_rng(A.bcz_hi, z0, ez);
+  auto xbc_in = [&](int gx0, int n) { return in_rng(A.bcx_lo, gx0, n) || in_rng(A.bcx_hi, gx0, n); };
 
   const int c = (tid / NQ2 < S::cells) ? tid / NQ2 : S::cells - 1;
   const int a = (tid / NQ) % NQ, b = tid % NQ;
@@ -1042,7 +1053,8 @@ BDX_PRAGMA_UNROLL(2)
     }
     __syncthreads();
 
-    auto do_gather = [&]() __attribute__((always_inline)) {
+    auto do_gather = [&](auto DIRC) __attribute__((always_inline)) {
+      constexpr bool DIR = decltype(DIRC)::value;
       // ------------------------------------------------ gather-sum and write out
       {
         const int64_t lbase = static_cast<int64_t>(cx) * P;
@@ -1074,7 +1086,7 @@ BDX_PRAGMA_UNROLL(2)
           // (and written) by the next segment
           if (red || (pl == P && !glast)) continue;
           const int gxx = cx * P + pl;
-          const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
+          const bool bc = DIR && ((m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi);
           const int kind = (m >> 4) & 3;
           if (bc) {
             if (kind == 0) continue;  // Dirichlet y was written at staging
@@ -1089,7 +1101,8 @@ BDX_PRAGMA_UNROLL(2)
       }
 
     };
-    auto do_stage_vec = [&]() __attribute__((always_inline)) {
+    auto do_stage_vec = [&](auto DIRC) __attribute__((always_inline)) {
+      constexpr bool DIR = decltype(DIRC)::value;
       // ------------------------------------------------ stage the next layer (VEC items)
       if (!last) {
 #pragma unroll
@@ -1109,6 +1122,7 @@ BDX_PRAGMA_UNROLL(2)
         auto dirichlet = [&](int m, int e, unsigned goff, T v) __attribute__((always_inline)) -> T {
           const int f = (m >> (4 * e)) & 15;
           const int gxx = (cx + 1) * P + ((m >> 16) & 15);
+          if constexpr (!DIR) return (f & kValid) ? v : T(0);
           if (!(f & kValid)) return T(0);
           if ((f & kBcYZ) || gxx == A.bcx_hi) {
             if (f & kOwnT) {
@@ -1173,7 +1187,8 @@ BDX_PRAGMA_UNROLL(2)
         }
       }
     };
-    auto do_stage = [&]() __attribute__((always_inline)) {
+    auto do_stage = [&](auto DIRC) __attribute__((always_inline)) {
+      constexpr bool DIR = decltype(DIRC)::value;
       // ------------------------------------------------ stage the next layer
       if (!last) {
         #pragma unroll
@@ -1203,7 +1218,7 @@ BDX_PRAGMA_UNROLL(2)
                   if (xupd) A.x[lnext + st_goff[k]] = pf_x[k] + xalpha * pf_p[k];
                 }
               }
-              if ((m & kBcYZ) || gxx == A.bcx_hi) {
+              if (DIR && ((m & kBcYZ) || gxx == A.bcx_hi)) {
                 if (m & kOwnT) {
                   const bool rown = (m & kRownYZ) && gxx < A.ownx;
                   yl[st_goff[k]] = rown ? val : T(0);
@@ -1233,11 +1248,27 @@ BDX_PRAGMA_UNROLL(2)
     // Consume the prefetch before the gather stores,
     // behind one explicit vmcnt(0) (as in lap_fused5.h)
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    if constexpr (VEC)
-      do_stage_vec();
+    // staging: planes 1..P of layer cx + 1; gather: planes 0..P of layer cx.
+    // As in lap_fused5.h the Q3 (ND = 4) instances keep the single copy (the
+    // split lost 1.5 % on the x-trilinear one; Q6 +0.3 %, profiles/r5_kernel_ab.md)
+    constexpr bool SPLIT = kF3DirSplit && (ND >= 6 || sizeof(T) == 4);
+    const bool dir_s = !SPLIT || tile_bc || xbc_in((cx + 1) * P + 1, P);
+    const bool dir_g = !SPLIT || tile_bc || xbc_in(cx * P, P + 1);
+    if constexpr (VEC) {
+      if (dir_s)
+        do_stage_vec(std::true_type{});
+      else
+        do_stage_vec(std::false_type{});
+    } else {
+      if (dir_s)
+        do_stage(std::true_type{});
+      else
+        do_stage(std::false_type{});
+    }
+    if (dir_g)
+      do_gather(std::true_type{});
     else
-      do_stage();
-    do_gather();
+      do_gather(std::false_type{});
     kc_cur = kc_nxt;
   }
   if constexpr (MODE == kFusedCG) {

@@ -44,6 +44,7 @@
 #pragma once
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "lap_fused2.h"
 
@@ -205,6 +206,16 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
   const int ez = (z0 + DZ <= Lz) ? DZ : Lz - z0;
   const int oy = top_y ? ey : TY * P;
   const int oz = top_z ? ez : TZ * P;
+  // Dirichlet nodes: the staging and the gather carry the identity-row work
+  // (y = r at Dirichlet dofs, zero columns) only where a tile holds a y / z
+  // boundary node or a layer an x boundary plane; both decisions are
+  // workgroup-uniform, so every other tile and layer runs a Dirichlet-free
+  // copy of the code, without the per-node branches (their exec-mask
+  // bookkeeping cost Q6 FP64 7 %, Q6 FP32 6 %, Q3 3 %: profiles/r5_kernel_ab.md)
+  auto in_rng = [](int v, int lo, int n) { return v >= lo && v < lo + n; };
+  const bool tile_bc = in_rng(A.bcy_lo, y0, ey) || in_rng(A.bcy_hi, y0, ey) ||
+                       in_rng(A.bcz_lo, z0, ez) || in_rng(A.bcz_hi, z0, ez);
+  auto xbc_in = [&](int gx0, int n) { return in_rng(A.bcx_lo, gx0, n) || in_rng(A.bcx_hi, gx0, n); };
 
   // lane roles: (cell of the wave, a, b); pass-dependent meaning of (a, b)
   const bool lane_on = lane < CPW * ND2;
@@ -701,7 +712,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
     }
     __syncthreads();
 
-    auto do_gather = [&]() __attribute__((always_inline)) {
+    auto do_gather = [&](auto DIRC) __attribute__((always_inline)) {
+      constexpr bool DIR = decltype(DIRC)::value;
       // ------------------------------------------------ gather-sum and write out
       {
   #pragma unroll
@@ -728,7 +740,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
           // (and written) by the next segment
           if (red || (pl == P && !glast)) continue;
           const int gxx = cx * P + pl;
-          const bool bc = (m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi;
+          const bool bc = DIR && ((m & kBcYZ) || gxx == A.bcx_lo || gxx == A.bcx_hi);
           const int kind = (m >> 4) & 3;
           if (bc) {
             if (kind == 0) continue;  // Dirichlet y was written at staging
@@ -745,7 +757,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
       }
 
     };
-    auto do_stage_vec = [&]() __attribute__((always_inline)) {
+    auto do_stage_vec = [&](auto DIRC) __attribute__((always_inline)) {
+      constexpr bool DIR = decltype(DIRC)::value;
       // ------------------------------------------------ stage the next layer (VEC items)
       if (!last) {
 #pragma unroll
@@ -765,6 +778,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
         auto dirichlet = [&](int m, int e, unsigned goff, T v) __attribute__((always_inline)) -> T {
           const int f = (m >> (4 * e)) & 15;
           const int gxx = (cx + 1) * P + ((m >> 16) & 15);
+          if constexpr (!DIR) return (f & kValid) ? v : T(0);
           if (!(f & kValid)) return T(0);
           if ((f & kBcYZ) || gxx == A.bcx_hi) {
             if (f & kOwnT) {
@@ -837,7 +851,8 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
         }
       }
     };
-    auto do_stage = [&]() __attribute__((always_inline)) {
+    auto do_stage = [&](auto DIRC) __attribute__((always_inline)) {
+      constexpr bool DIR = decltype(DIRC)::value;
       // ------------------------------------------------ stage the next layer
       if (!last) {
   #pragma unroll
@@ -873,7 +888,7 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
                   }
                 }
               }
-              if ((m & kBcYZ) || gxx == A.bcx_hi) {
+              if (DIR && ((m & kBcYZ) || gxx == A.bcx_hi)) {
                 if (m & kOwnT) {
                   const bool rown = (m & kRownYZ) && gxx < A.ownx;
                   yl[st_goff[k]] = rown ? val : T(0);
@@ -908,11 +923,27 @@ __global__ void __launch_bounds__((F5Shape<T, ND>::NT), (f5_waves<T, ND, MODE>()
     // pass sees nothing outstanding and does not put a draining wait before
     // each slot's stores.
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    if constexpr (VEC)
-      do_stage_vec();
+    // staging: planes 1..P of layer cx + 1; gather: planes 0..P of layer cx.
+    // Q3 (ND = 4) keeps the single Dirichlet-aware copy: the split measured
+    // 1.4 % slower there (profiles/r5_kernel_ab.md)
+    constexpr bool SPLIT = ND >= 6 || sizeof(T) == 4;
+    const bool dir_s = !SPLIT || tile_bc || xbc_in((cx + 1) * P + 1, P);
+    const bool dir_g = !SPLIT || tile_bc || xbc_in(cx * P, P + 1);
+    if constexpr (VEC) {
+      if (dir_s)
+        do_stage_vec(std::true_type{});
+      else
+        do_stage_vec(std::false_type{});
+    } else {
+      if (dir_s)
+        do_stage(std::true_type{});
+      else
+        do_stage(std::false_type{});
+    }
+    if (dir_g)
+      do_gather(std::true_type{});
     else
-      do_stage();
-    do_gather();
+      do_gather(std::false_type{});
     kc_cur = kc_nxt;
   }
   if constexpr (MODE == kFusedCG) {
