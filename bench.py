@@ -75,6 +75,9 @@ def parse_args(argv=None):
                          "(general trilinear) mesh, the "
                          "reference's data model (dofmap + stored G, Q3 and Q6) and Q6 "
                          "perturbed (GPU only; auto: on for one rank)")
+    ap.add_argument("--box-probe", default="on", choices=["on", "off"],
+                    help="after every timed run, measure the box's HBM stream rate "
+                         "(untimed context: config.box_stream)")
     return ap.parse_args(argv)
 
 
@@ -257,7 +260,7 @@ def _measure_isolated(a, config, steps, warmup, *, kappa="constant", perturb=0.0
 
     argv = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--config", config,
             "--steps", str(steps), "--warmup", str(warmup), "--companions", "off",
-            "--extras", "off", "--profile-steps", "0", "--kappa", kappa,
+            "--extras", "off", "--box-probe", "off", "--profile-steps", "0", "--kappa", kappa,
             "--perturb", repr(float(perturb)), "--kernel", kernel, "--geometry", geometry,
             "--platform", a.platform]
     if a.dofs_per_gpu:
@@ -406,9 +409,41 @@ def run(comm, a) -> dict | None:
                         comm, a, cfg, a.steps, a.warmup, log=log, **kw), log)
             except Exception as e:
                 raise MeasurementFailed(f"{key}: {e!r}", (head, companions, extras)) from e
+    if gpu and a.box_probe == "on":
+        try:
+            head["box_stream"] = _guarded(comm, lambda: _stream_probe(comm, head["dofs_per_gpu"]),
+                                          log)
+        except Exception as e:
+            raise MeasurementFailed(f"box_stream: {e!r}", (head, companions, extras)) from e
     if comm.rank != 0:
         return None
     return _record(a, n, head, companions, extras, flags, gpu)
+
+
+def _stream_probe(comm, n: int, reps: int = 10) -> dict:
+    """The box's HBM stream rate, measured after every timed run (context, not
+    part of any timed region): r += a y over the headline's n doubles per GPU,
+    2 reads + 1 write, the CG update pass's access pattern.  Boxes of this pool
+    differ by 7-12 % on the stream-bound configs (Q3, the dofmap data model)
+    while the compute-side Q6 ones do not (profiles/r5_final_repeat.md); this
+    puts the box's rate next to the number.  TB/s, min / max over ranks."""
+    import torch
+    r = torch.ones(n, dtype=torch.float64, device="cuda")
+    y = torch.ones_like(r)
+    r.add_(y, alpha=-1e-9)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        r.add_(y, alpha=-1e-9)
+    e1.record()
+    torch.cuda.synchronize()
+    tbps = 24.0 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    del r, y
+    torch.cuda.empty_cache()
+    return {"op": "r += a*y, fp64, 2R1W", "n": n,
+            "tbps_min": -comm.allreduce_scalar(-tbps, "max"),
+            "tbps_max": comm.allreduce_scalar(tbps, "max")}
 
 
 def _record(a, n, head, companions, extras, flags, gpu) -> dict:
@@ -454,6 +489,7 @@ def _record(a, n, head, companions, extras, flags, gpu) -> dict:
             "phases_ms": head.get("phases_ms"),
             "phases_ms_max_over_ranks": head.get("phases_ms_max_over_ranks"),
             "phases_per_rank": head.get("phases_per_rank"),
+            "box_stream": head.get("box_stream"),
         },
         "q6_gdofs": companions.get("q6", {}).get("value"),
         "q6f32_gdofs": companions.get("q6f32", {}).get("value"),
