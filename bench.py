@@ -134,6 +134,9 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
     mark("rhs")
     op = make_operator(pb, kernel, geometry)
     mark("operator")
+    # one operator action on the RHS before the CG (untimed): the
+    # cross-family consistency check of _record compares these scalars
+    check = _action_check(pb, op, u) if gpu else None
 
     def sync():
         if gpu:
@@ -206,6 +209,7 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
         "kappa": kappa,
         "geom_perturb_fact": perturb,
         "y_norm": ynorm,
+        "action_check": check,
         "setup_s": t_setup,
         "setup_phases_s": phase_t,
         "runtime": (f"native C++ ({rt.transport}, hipGraph={rt.graphs}, overlap={rt.overlap}, "
@@ -250,6 +254,83 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
     return rec
 
 
+def _emulated_prediction(config: str, kernel: str, n: int):
+    """ms per step that one rank of this N-rank run measured ALONE on one GPU
+    with modelled 50 GB/s + 10 us links (scripts/emulate_rank.py, committed in
+    benchmark_dolfinx_amd/data/emulated_predictions.json): context for the
+    first real multi-GPU curve, never part of a timed value.  None if that
+    (config, kernel, N) was not emulated."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "benchmark_dolfinx_amd",
+                        "data", "emulated_predictions.json")
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+        return tab["runs"][config][kernel][str(n)]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def _action_check(pb, op, u) -> dict:
+    """z = A b once (the operator's action mode, before any CG state exists)
+    and two scalars of it: ||z||_2 and <z, w> with w_i = sin(0.7 i + 0.3) over
+    the storage index (owned dofs).  Families that implement the same
+    operator on the same partition must agree to rounding (~1e-14); unlike the
+    CG iterate's norm, which drifts with the summation order over hundreds of
+    iterations (Q6 at 210 iterations: 5e-6 between two runs of the SAME
+    kernel on different boxes, profiles/r5*_bench_default.json), this pins
+    the operator itself."""
+    import torch
+    z = pb.new_vector()
+    op.apply(u, z)
+    torch.cuda.synchronize()
+    w = torch.sin(torch.arange(z.numel(), dtype=torch.float64, device=z.device) * 0.7 + 0.3)
+    w = w.view(z.shape)
+    out = {"norm": pb.norm(z), "wdot": pb.inner(z, w)}
+    del z, w
+    torch.cuda.empty_cache()
+    return out
+
+
+# Pairs of records that time the same problem with different operator
+# families (headline / companion key, variant key): their action checks must
+# agree to CONSISTENCY_TOL, else the run fails (VERDICT r5 item 5).
+CONSISTENCY_PAIRS = (("q3", "dofmap"), ("q6", "q6_dofmap"), ("general", "general_trilinear"))
+CONSISTENCY_TOL = 1e-9
+YNORM_TOL = 1e-4  # CG iterates: rounding drift over hundreds of iterations (see above)
+
+
+def _consistency(head, companions, extras) -> dict:
+    """Relative gaps of the action checks and of the CG iterate norms for the
+    CONSISTENCY_PAIRS present in this run; `ok` is False if any gap exceeds
+    its tolerance (action: 1e-9 in FP64, 1e-5 in FP32; y_norm: 1e-4)."""
+    recs = {"q3": head if head.get("degree") == 3 else None, **companions, **extras}
+    if head.get("degree") == 6:
+        recs.setdefault("q6", head)
+    out = {"tol_action": CONSISTENCY_TOL, "tol_y_norm": YNORM_TOL, "pairs": {}, "ok": True}
+    for a_key, b_key in CONSISTENCY_PAIRS:
+        ra, rb = recs.get(a_key), recs.get(b_key)
+        if not ra or not rb or ra.get("value") is None or rb.get("value") is None:
+            continue
+        ca, cb = ra.get("action_check"), rb.get("action_check")
+        if ra.get("geom_perturb_fact") != rb.get("geom_perturb_fact") or \
+                ra.get("kappa") != rb.get("kappa"):
+            continue
+        gaps = {}
+        if ca and cb:
+            for k in ("norm", "wdot"):
+                gaps[f"action_{k}"] = abs(ca[k] - cb[k]) / max(abs(cb[k]), 1e-300)
+        if ra.get("y_norm") is not None and rb.get("y_norm") is not None and \
+                ra.get("steps") == rb.get("steps") and ra.get("warmup") == rb.get("warmup"):
+            gaps["y_norm"] = abs(ra["y_norm"] - rb["y_norm"]) / max(abs(rb["y_norm"]), 1e-300)
+        tol = CONSISTENCY_TOL if ra.get("dtype", "fp64") == "fp64" else 1e-5
+        ok = all(v <= (YNORM_TOL if k == "y_norm" else tol) for k, v in gaps.items())
+        out["pairs"][f"{a_key}~{b_key}"] = {
+            "kernels": [ra.get("kernel"), rb.get("kernel")],
+            **{k: float(f"{v:.3e}") for k, v in gaps.items()}, "ok": ok}
+        out["ok"] = out["ok"] and ok
+    return out
+
+
 def _measure_isolated(a, config, steps, warmup, *, kappa="constant", perturb=0.0,
                       kernel="auto", geometry="auto", log=None) -> dict:
     """One-rank `_measure` in a child interpreter (this script, headline only,
@@ -290,6 +371,7 @@ def _measure_isolated(a, config, steps, warmup, *, kappa="constant", perturb=0.0
             "ndofs_global": c["global_batch"], "mesh": c["mesh"], "kernel": c["kernel"],
             "geometry": c["geometry"], "x_segments": c["x_segments"], "kappa": c["kappa"],
             "geom_perturb_fact": c["geom_perturb_fact"], "y_norm": c["y_norm"],
+            "action_check": c.get("action_check"),
             "setup_s": c["setup_s"], "runtime": c["runtime"], "isolated_process": True}
 
 
@@ -370,7 +452,21 @@ def run(comm, a) -> dict | None:
             except Exception as e:
                 raise MeasurementFailed(f"{key}: {e!r}", (head, companions, {})) from e
     extras = {}
-    if gpu and (a.extras == "on" or (a.extras == "auto" and n == 1)):
+    if gpu and a.extras == "auto" and n > 1 and a.config == "q3" and not a.mesh:
+        # N > 1: the reference's own data model (dofmap + stored G, the
+        # layout of its published 64-rank runs, /root/reference/src/
+        # laplacian.hpp:281-349) on this weak-scaled mesh, in-process after
+        # the companions, at the headline's steps / warm-up, with its per-rank
+        # split-schedule timeline
+        try:
+            extras["dofmap"] = _guarded(comm, lambda: _measure(
+                comm, a, a.config, a.steps, a.warmup, kappa=a.kappa, perturb=a.perturb,
+                kernel="dofmap", geometry="stored", profile_steps=a.profile_steps, log=log), log)
+        except Exception as e:
+            raise MeasurementFailed(f"dofmap: {e!r}", (head, companions, extras)) from e
+        if extras["dofmap"].get("value") is not None:
+            extras["dofmap"]["emulated_ms_per_step"] = _emulated_prediction(a.config, "dofmap", n)
+    elif gpu and (a.extras == "on" or (a.extras == "auto" and n == 1)):
         # north-star variants of the headline config (BASELINE.json: random
         # coefficients; the reference's --geom_perturb_fact general cells; the
         # reference's own data model).  "general" takes the auto kernel
@@ -387,7 +483,11 @@ def run(comm, a) -> dict | None:
                                            geometry="stored")),
                  ("q6_general", "q6", dict(kappa=a.kappa, perturb=pert)),
                  ("q6_dofmap", "q6", dict(kappa=a.kappa, perturb=a.perturb, kernel="dofmap",
-                                          geometry="stored")))
+                                          geometry="stored")),
+                 # BASELINE configs[4] "MFMA f32 tensor contractions": fused3's
+                 # FP32 x-trilinear instance, whose y / z stages run on
+                 # v_mfma_f32_16x16x4_f32 (lap_fused3.h kF3MfmaF32)
+                 ("q6f32_general", "q6f32", dict(kappa=a.kappa, perturb=pert)))
         # Each variant runs in a fresh child process on one rank: in this
         # process, after the headline and the 500 M DoF companions, the
         # variants measured up to 15 % low (dofmap Q3 11.9 vs 14.0 GDoF/s on
@@ -481,6 +581,7 @@ def _record(a, n, head, companions, extras, flags, gpu) -> dict:
             "runtime": head["runtime"],
             "per_gpu_gdofs": head["value"] / n,
             "y_norm": head["y_norm"],
+            "action_check": head.get("action_check"),
             "setup_s": head["setup_s"],
             "setup_phases_s": head["setup_phases_s"],
             "device": _device_name() if gpu else "cpu",
@@ -490,6 +591,8 @@ def _record(a, n, head, companions, extras, flags, gpu) -> dict:
             "phases_ms_max_over_ranks": head.get("phases_ms_max_over_ranks"),
             "phases_per_rank": head.get("phases_per_rank"),
             "box_stream": head.get("box_stream"),
+            "emulated_ms_per_step": (_emulated_prediction(a.config, head["kernel"], n)
+                                     if n > 1 else None),
         },
         "q6_gdofs": companions.get("q6", {}).get("value"),
         "q6f32_gdofs": companions.get("q6f32", {}).get("value"),
@@ -500,7 +603,9 @@ def _record(a, n, head, companions, extras, flags, gpu) -> dict:
         "dofmap_gdofs": extras.get("dofmap", {}).get("value"),
         "q6_general_gdofs": extras.get("q6_general", {}).get("value"),
         "q6_dofmap_gdofs": extras.get("q6_dofmap", {}).get("value"),
+        "q6f32_general_gdofs": extras.get("q6f32_general", {}).get("value"),
         "variants": extras,
+        "consistency": _consistency(head, companions, extras),
     }
 
 
@@ -650,10 +755,17 @@ def main(argv=None) -> int:
             print(json.dumps(rec), flush=True)
         print(f"bench.py: rank {comm.rank}: {e!r}", file=sys.stderr, flush=True)
         return 1
+    rc = 0
     if line is not None:
         print(json.dumps(line), flush=True)
+        cons = line.get("consistency") or {}
+        if not cons.get("ok", True):
+            bad = {k: v for k, v in cons["pairs"].items() if not v["ok"]}
+            print(f"bench.py: operator families disagree on the same problem: {bad}",
+                  file=sys.stderr, flush=True)
+            rc = 4
     finalize()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
 // Fused-kernel helpers: tile query, table packing, the interface-partials
 // finalize pass and the fused2/3 CG update.
+#include <cstdlib>
 #include "lap_fused3.h"
 
 // Packed 1D tables of the fused kernel (layout: FusedShape::OFF_*), written
@@ -493,8 +494,12 @@ BDX_CGI(float, f32)
     const int64_t nvec = L.size() / (16 / static_cast<int64_t>(sizeof(T)));                    \
     const int64_t want = (nvec + 256 * kUpdU - 1) / (256 * kUpdU);                             \
     const int g = static_cast<int>(want < kUpdGrid ? (want > 0 ? want : 1) : kUpdGrid); \
-    /* interface partials prefetched (byte offsets of the buffers fit 31 bits) */          \
-    const bool pre = kUpdPre && L.L[0] * L.L[1] * (ntz > 1 ? ntz - 1 : 1) * 8 < (1LL << 31) &&  \
+    /* interface partials prefetched (byte offsets of the buffers fit 31 bits); the   */      \
+    /* plain kernel serves larger blocks (BDX_UPD_PLAIN=1 forces it: the test hook of */      \
+    /* tests/test_gpu_runtime.py::test_tiled_update_plain_path_matches)               */      \
+    const bool force_plain = std::getenv("BDX_UPD_PLAIN") != nullptr;                         \
+    const bool pre = kUpdPre && !force_plain &&                                                \
+                     L.L[0] * L.L[1] * (ntz > 1 ? ntz - 1 : 1) * 8 < (1LL << 31) &&            \
                      L.L[0] * (nty > 1 ? nty - 1 : 1) * L.L[2] * 8 < (1LL << 31);              \
     if (pre && sizeof(T) == 4 && L.tsz % 4 == 0)                                               \
       cg_update_tiled_pre_kernel<T, true, kUpdU><<<g, 256, 0, st>>>(                           \

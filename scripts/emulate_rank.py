@@ -53,6 +53,9 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--profile-steps", type=int, default=10)
     ap.add_argument("--no-single", action="store_true", help="skip the 1-rank comparison")
+    ap.add_argument("--kernel", default="auto", help="operator family (dofmap: the reference's "
+                    "data model, with --geometry stored)")
+    ap.add_argument("--geometry", default="auto")
     a = ap.parse_args(argv)
     degree, dpg, _, _ = bench.CONFIGS[a.config]
     nx = compute_mesh_size(dpg * a.ranks, degree)
@@ -84,7 +87,7 @@ def main(argv=None) -> int:
 
     comm = EmulatedRankComm(rank, a.ranks)
     rec = bench._measure(comm, ba, a.config, a.steps, a.warmup, profile_steps=a.profile_steps,
-                         log=log)
+                         kernel=a.kernel, geometry=a.geometry, log=log)
     ph = rec.get("phases_ms") or {}
     out = {"mode": "emulated", "config": a.config, "nranks": a.ranks, "rank": rank,
            "mesh_global": list(nx), "block_cells": list(block), "ghost_planes": list(lat.gh),
@@ -100,7 +103,8 @@ def main(argv=None) -> int:
     if not a.no_single:
         ba1 = bench.parse_args(["--config", a.config, "--mesh", ",".join(map(str, block))])
         r1 = bench._measure(Comm(), ba1, a.config, a.steps, a.warmup,
-                            profile_steps=a.profile_steps, log=log)
+                            profile_steps=a.profile_steps, kernel=a.kernel,
+                            geometry=a.geometry, log=log)
         print(json.dumps({"mode": "single", "config": a.config, "block_cells": list(block),
                           "ms_per_step": r1["ms_per_step"],
                           "ms_per_step_median": r1["ms_per_step_median"],

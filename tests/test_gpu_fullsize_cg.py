@@ -11,6 +11,11 @@ norms must agree to 1e-10: the fused CG reorganisation (p formed in the
 operator's staging, x lagged by one iteration, tile-interface partials folded
 in the update pass) is exact arithmetic reordering, so only rounding may differ.
 The stored-G v1 operator needs ~67 GB (Q3) / ~57 GB (Q6) of HBM.
+
+Round 6: the iterate VECTORS are compared, not only their
+norms: max |x_prod - x_ref| / max |x_ref| <= 1e-10, for the reference-layout
+`v1` kernel and for the reference data model (`dofmap`: cell -> dof map,
+stored G, atomic scatter).
 """
 
 import pytest
@@ -33,12 +38,11 @@ def _solve(pb, u, kernel, geometry, nits):
     cg.solve(op, x, u, nits)
     cg.wait()
     torch.cuda.synchronize()
-    xn = pb.norm(x)
     if hasattr(op, "close"):
         op.close()
-    del op, cg, x
+    del op, cg
     torch.cuda.empty_cache()
-    return xn, name
+    return pb.owned(x).clone(), name
 
 
 @pytest.mark.parametrize("degree,ndofs,kernel,prod", [(3, 300_000_000, "auto", "fused5"),
@@ -49,10 +53,17 @@ def test_fullsize_cg_iterate_production_vs_stored_geometry(degree, ndofs, kernel
     pb = PoissonProblem(Comm(), nx, degree, 1, False, torch.float64, "gpu")
     u = pb.assemble_rhs()
     x_prod, name_prod = _solve(pb, u, kernel, "auto", 20)
-    x_ref, name_ref = _solve(pb, u, "v1", "stored", 20)
     assert name_prod == prod, name_prod
-    assert name_ref != name_prod
-    rel = abs(x_prod - x_ref) / abs(x_ref)
-    print(f"Q{degree} {pb.ndofs_global} DoFs: {name_prod} {x_prod!r} vs {name_ref} {x_ref!r} "
-          f"(rel {rel:.2e})")
-    assert rel <= 1e-10, (x_prod, x_ref, rel)
+    xmax = float(torch.max(torch.abs(x_prod)))
+    for ref_kernel in ("v1", "dofmap"):
+        x_ref, name_ref = _solve(pb, u, ref_kernel, "stored", 20)
+        assert name_ref != name_prod
+        rel = float(torch.max(torch.abs(x_prod - x_ref))) / xmax
+        nrel = abs(float(torch.linalg.vector_norm(x_prod)) / float(torch.linalg.vector_norm(x_ref))
+                   - 1.0)
+        print(f"Q{degree} {pb.ndofs_global} DoFs: {name_prod} vs {name_ref}: max|dx|/max|x| "
+              f"{rel:.2e}, norm rel {nrel:.2e}")
+        assert rel <= 1e-10, (name_ref, rel)
+        assert nrel <= 1e-10, (name_ref, nrel)
+        del x_ref
+        torch.cuda.empty_cache()

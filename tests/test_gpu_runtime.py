@@ -320,3 +320,22 @@ def test_tiled_storage_fused3_general(monkeypatch, P, nc, dtype, coef, pert, ran
         assert t1 is (dtype == torch.float64 or P % 2 == 0) and t0 is False
         assert abs(a1 - b1) <= tol * abs(b1), (a1, b1)
         assert abs(a2 - b2) <= tol * abs(b2), (a2, b2)
+
+
+@pytest.mark.parametrize("P,nc,dtype", [(3, (5, 13, 7), torch.float64), (6, (3, 5, 6), torch.float32)])
+def test_tiled_update_plain_path_matches(monkeypatch, P, nc, dtype):
+    """The tiled update pass's plain kernel (interface partials loaded inside
+    their branches; the production path for blocks whose interface buffers
+    pass 2^31 bytes) against the prefetching one: same sums in the same order,
+    so the CG iterates agree to rounding (the path had no
+    test).  BDX_UPD_PLAIN=1 forces it on these small meshes."""
+    monkeypatch.setenv("BDX_TILED", "1")
+    monkeypatch.setenv("BDX_UPD_PLAIN", "1")
+    got = run_threaded(1, _tiled_job, nc, P, 12, 5, dtype, "random")
+    monkeypatch.delenv("BDX_UPD_PLAIN")
+    ref = run_threaded(1, _tiled_job, nc, P, 12, 5, dtype, "random")
+    tol = 1e-13 if dtype == torch.float64 else 1e-6
+    for (a1, a2, t1), (b1, b2, t0) in zip(got, ref):
+        assert t1 is True and t0 is True
+        assert abs(a1 - b1) <= tol * abs(b1), (a1, b1)
+        assert abs(a2 - b2) <= tol * abs(b2), (a2, b2)
