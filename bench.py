@@ -272,8 +272,9 @@ def _emulated_prediction(config: str, kernel: str, n: int):
 
 def _action_check(pb, op, u) -> dict:
     """z = A b once (the operator's action mode, before any CG state exists)
-    and two scalars of it: ||z||_2 and <z, w> with w_i = sin(0.7 i + 0.3) over
-    the storage index (owned dofs).  Families that implement the same
+    and two scalars of it: ||z||_2 and sum_i w_i z_i^2 with w_i = 1 + sin(0.7 i
+    + 0.3) / 2 over the storage index (owned dofs; positive weights, so the
+    sum does not cancel and a misplaced entry changes it).  Families that implement the same
     operator on the same partition must agree to rounding (~1e-14); unlike the
     CG iterate's norm, which drifts with the summation order over hundreds of
     iterations (Q6 at 210 iterations: 5e-6 between two runs of the SAME
@@ -283,8 +284,9 @@ def _action_check(pb, op, u) -> dict:
     z = pb.new_vector()
     op.apply(u, z)
     torch.cuda.synchronize()
-    w = torch.sin(torch.arange(z.numel(), dtype=torch.float64, device=z.device) * 0.7 + 0.3)
-    w = w.view(z.shape)
+    w = 1.0 + 0.5 * torch.sin(torch.arange(z.numel(), dtype=torch.float64, device=z.device) * 0.7
+                              + 0.3)
+    w = w.view(z.shape) * z.double()
     out = {"norm": pb.norm(z), "wdot": pb.inner(z, w)}
     del z, w
     torch.cuda.empty_cache()

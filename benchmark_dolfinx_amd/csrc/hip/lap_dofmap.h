@@ -736,6 +736,20 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   }
 }
 
+#include "lap_dofmfma.h"
+
+// Which operator kernel the dofmap launches take in FP64 where both exist
+// (nd <= 8, nq <= 8): the MFMA one (lap_dofmfma.h) or the line-per-lane VALU
+// one above.  BDX_DOFMAP_MFMA=1 / 0 forces it (A/B builds and tests); unset:
+// kDofMfmaDefault(nq).  bdx_dofmap_set_mfma() overrides both (-1: back to
+// the environment / default).
+extern "C" int bdx_dofmap_set_mfma(int mode);
+int bdx_dofmap_mfma_mode();
+// Round 6, same box, bench.py --kernel dofmap --geometry stored, GDoF/s (VALU
+// / MFMA): Q3 14.47 / 10.74, Q6 22.79 / 21.31 (profiles/r6_dofmap_mfma.md):
+// the VALU kernel stays the default.
+constexpr bool kDofMfmaDefault(int nq) { return nq < 0; }
+
 // Stored G in the reference layout for a cell list (geometry_computation_gpu,
 // src/geometry_gpu.hpp:26-132): one thread per (cell, quadrature point).
 template <typename T, int NQ>
@@ -883,6 +897,19 @@ int launch_dofmap(int geom, int mode, DofArgs<T> a, int* nblocks, hipStream_t st
   const int nb = dofmap_blocks<NQ>(a.ncl, &a.cells_per_block);
   *nblocks = nb;
   constexpr int NT = DofShape<NQ>::NT;
+  if constexpr (sizeof(T) == 8 && ND <= 8 && NQ <= 8) {
+    const int mm = bdx_dofmap_mfma_mode();
+    if (mm == 1 || (mm < 0 && kDofMfmaDefault(NQ))) {
+      static_assert(DofMfmaShape<ND, NQ>::NT == NT && NT == 256, "block shape of the VALU kernel");
+#define BDX_DM(G, M) lap_dofmfma_kernel<ND, NQ, G, M><<<nb, NT, 0, st>>>(a)
+      if (geom == kGeomStored)
+        (mode == kDofCG) ? BDX_DM(kGeomStored, kDofCG) : BDX_DM(kGeomStored, kDofAction);
+      else
+        (mode == kDofCG) ? BDX_DM(kGeomOTF, kDofCG) : BDX_DM(kGeomOTF, kDofAction);
+#undef BDX_DM
+      return static_cast<int>(hipGetLastError());
+    }
+  }
 #define BDX_DL(G, M) lap_dofmap_kernel<T, ND, NQ, G, M><<<nb, NT, 0, st>>>(a)
   if (geom == kGeomStored)
     (mode == kDofCG) ? BDX_DL(kGeomStored, kDofCG) : BDX_DL(kGeomStored, kDofAction);

@@ -1,6 +1,22 @@
 // dofmap (unstructured data model) operator, double instantiations.
+#include <cstdlib>
+
 #include "lap_dofmap.h"
 BDX_DOFMAP_API(double, f64)
+
+// kernel choice of the FP64 dofmap launches (lap_dofmap.h): -1 = environment
+// (BDX_DOFMAP_MFMA) / default, 0 = VALU kernel, 1 = MFMA kernel
+static int g_dofmap_mfma = -1;
+extern "C" int bdx_dofmap_set_mfma(int mode) {
+  g_dofmap_mfma = mode < 0 ? -1 : (mode ? 1 : 0);
+  return 0;
+}
+int bdx_dofmap_mfma_mode() {
+  if (g_dofmap_mfma >= 0) return g_dofmap_mfma;
+  const char* e = std::getenv("BDX_DOFMAP_MFMA");
+  if (e && *e) return std::atoi(e) ? 1 : 0;
+  return -1;
+}
 
 // Writer designation of the dofmap CG (type independent): the first
 // occurrence of every dof over the launch order [cells_a..., cells_b...]

@@ -73,6 +73,7 @@ def declare(lib) -> None:
     _d(lib, "bdx_rt_create_dofmap", [i32, vp, vp, i64, f64, vp, vp, vp, vp, i32, i32, i32, i64,
                                      vp], vp)
     _d(lib, "bdx_dofmap_nblocks", [i32, i32])
+    _d(lib, "bdx_dofmap_set_mfma", [i32])
     _d(lib, "bdx_rt_tiled", [vp])
     _d(lib, "bdx_rt_connect", [vp, vp, i32])
     _d(lib, "bdx_rt_comm_count", [vp])

@@ -73,10 +73,15 @@ class HipKernels:
                                        ptr(hi), _stream()), "v1_apply")
 
     def dofmap_tables(self, device):
-        """Device copy of the 1D tables the dofmap kernel reads as scalar loads:
-        [phi0 (nq x nd) | dphi1 (nq x nq) | qpts | wts] in the vector dtype."""
+        """Device copy of the 1D tables the dofmap kernels read:
+        [phi0 (nq x nd) | dphi1 (nq x nq) | qpts | wts | Dd = dphi1 phi0 (nq x nd) |
+        phi0^T | Dd^T] in the vector dtype (Dd and the transposes: the MFMA kernel,
+        lap_dofmfma.h)."""
         t = self.t
-        h = np.concatenate([t.phi0.ravel(), t.dphi1.ravel(), t.qpts.ravel(), t.wts.ravel()])
+        dd = np.asarray(t.dphi1, dtype=np.float64) @ np.asarray(t.phi0, dtype=np.float64)
+        h = np.concatenate([t.phi0.ravel(), t.dphi1.ravel(), t.qpts.ravel(), t.wts.ravel(),
+                            dd.ravel(), np.ascontiguousarray(t.phi0.T).ravel(),
+                            np.ascontiguousarray(dd.T).ravel()])
         return torch.from_numpy(h).to(device, self.dtype)
 
     def dofmap_apply(self, geom: int, tab, cells, ncl: int, cdofs, cverts, coords, flags, G,

@@ -16,6 +16,18 @@ from benchmark_dolfinx_amd.solvers.cg import DeviceCG, cg_solve
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(params=["valu", "mfma"], autouse=True)
+def dofmap_kernel(request):
+    """Every test runs on both FP64 operator kernels of the data model: the
+    line-per-lane VALU kernel (lap_dofmap.h) and the MFMA one
+    (lap_dofmfma.h); FP32 always takes the VALU kernel."""
+    from benchmark_dolfinx_amd.ops import native
+    lib = native.hip()
+    lib.bdx_dofmap_set_mfma(1 if request.param == "mfma" else 0)
+    yield request.param
+    lib.bdx_dofmap_set_mfma(-1)
+
 CASES = [
     # ncells, P, qmode, gauss, perturb, dtype, kappa
     ((3, 3, 3), 3, 0, False, 0.0, torch.float64, "constant"),
