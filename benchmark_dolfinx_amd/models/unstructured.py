@@ -22,6 +22,7 @@ and the CG solvers are shared with the structured operators.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -149,6 +150,11 @@ class DofmapLaplacianGPU:
             self.coords = torch.from_numpy(m.coords).to(dev, dt)
             self.flags = torch.from_numpy(m.dof_flags).to(dev)
             self.tab = self.k.dofmap_tables(dev)
+            if os.environ.get("BDX_TEST_CORRUPT_DOFMAP"):
+                # test hook (tests/test_gpu_bench_consistency.py): a 0.1 % error
+                # in one interpolation entry, which bench.py's cross-family
+                # consistency gate must catch
+                self.tab[0] *= 1.001
             self.inner = torch.from_numpy(m.interior_cells).to(dev)
             self.outer = torch.from_numpy(m.boundary_cells).to(dev)
             self.kc = None if m.kc is None else torch.from_numpy(m.kc).to(dev, dt)
