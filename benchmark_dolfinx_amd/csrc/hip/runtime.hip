@@ -602,6 +602,14 @@ struct LoopBase {
   //   maskr as mask, and the comm stream is confined to the reserved CUs.
   // The reserved CUs are mask bits 0 .. reserve-1, which the hardware deals
   // round-robin over the XCDs (csrc/micro/dispatch_prio.hip census).
+  // hipExtStreamCreateWithCUMask takes no flags or priority: si (mask, maskr)
+  // and the re-created cs (maskr) are BLOCKING streams at the DEFAULT
+  // priority, unlike the non-blocking greatest-priority cs of init_common.
+  // So in maskr the comm chain loses its priority, and both streams
+  // synchronise with the legacy null stream: any work the caller submits to
+  // the null stream while iterate() runs serialises with them.  The mask /
+  // maskr A/Bs (profiles/r5_split_schedule.md) ran with nothing on the null
+  // stream; comm_priority() reports the priority cs really has.
   int make_interior_stream() {
     const char* e = std::getenv("BDX_SPLIT");
     const std::string mode = e ? e : "prio";
@@ -1263,6 +1271,13 @@ struct DofCGRuntime final : LoopBase {
   // streams r, y and r back and no longer writes y = 0 (one vector stream
   // less per iteration; the zero stores ride in the operator's tail).  y2 is
   // the runtime's own second buffer; y (the caller's) is yk of even k.
+  // Invariant: after iterate() the caller's y holds A p of the last even
+  // iteration (NOT zero) and y2 may be dirty.  Only reset() (called by
+  // DofmapLaplacianGPU.cg_start, which zeroes the caller's y first) makes
+  // the loop valid again: iteration 0 then adds into a zero y and zeroes y2
+  // before iteration 1 adds into it.  No caller may read y after iterate()
+  // or hand the solve to the Python driver mid-way without cg_start
+  // (tests/test_gpu_dofmap.py::test_dofmap_native_second_solve_*).
   T* y2 = nullptr;
   T* yk(long k) const { return (k % 2 == 0) ? y : y2; }
 

@@ -147,3 +147,34 @@ def test_dofmap_cg_matches_host_cg(nc, P, qm, geometry, dt, kappa, runtime):
     tol = 1e-10 if dt == torch.float64 else 2e-4
     xo, xr = cpu.owned(xg.double().cpu()), cpu.owned(xc)
     assert (xo - xr).abs().max().item() <= tol * xr.abs().max().item()
+
+
+@pytest.mark.parametrize("first", [6, 7])
+def test_dofmap_native_second_solve_after_even_and_odd_counts(first):
+    """the native runtime's y ping-pong leaves the caller's y
+    holding A p of the last even iteration.  A second solve on the same
+    operator / DeviceCG (the reset path) after an even and after an odd
+    iteration count must equal a fresh solve, even with cg.y overwritten in
+    between (cg_start zeroes it; nothing may rely on it after iterate)."""
+    pb = PoissonProblem(Comm(), (4, 3, 5), 3, 1, False, torch.float64, "gpu", 0.1, "random")
+    u = pb.assemble_rhs()
+    op = DofmapLaplacianGPU(pb, "stored")
+    cg = DeviceCG(pb)
+    x1 = pb.new_vector()
+    cg.solve(op, x1, u, first)
+    cg.wait()
+    assert op._rt is not None
+    cg.y.fill_(1e300)  # garbage in the caller's y between the solves
+    x2 = pb.new_vector()
+    cg.solve(op, x2, u, 9)
+    cg.wait()
+    op.close()
+    ref_op = DofmapLaplacianGPU(pb, "stored")
+    ref_cg = DeviceCG(pb)
+    x3 = pb.new_vector()
+    ref_cg.solve(ref_op, x3, u, 9)
+    ref_cg.wait()
+    ref_op.close()
+    torch.cuda.synchronize()
+    d = (pb.owned(x2) - pb.owned(x3)).abs().max().item()
+    assert d <= 1e-11 * pb.owned(x3).abs().max().item(), d  # float atomics: rounding only
