@@ -151,14 +151,36 @@ inline void interp_t(const Tables<T>& tb, const T* r, T* ye, T* t1, T* t2) {
 // y += kappa * A_cell u for one cell, BC semantics of the reference
 // (src/laplacian_gpu.hpp:153-170, 424-425): BC inputs are zeroed, BC outputs
 // get y = u (only on the owning rank).
+// Compile-time extents (the loops unroll and the innermost axis -- contiguous
+// qz or the NQ^2 plane -- vectorises) and, when the caller precomputed them,
+// the geometry factors G[6][nq^3] of the cell in the reference layout
+// (src/geometry_cpu.hpp; computed once per operator by bdx_cpu_geometry, as
+// the reference's MatFreeLaplacianCPU does, src/laplacian.hpp:515-541).
+// Gc == nullptr: per-point trilinear geometry.  Round 6: this replaced a
+// runtime-extent version (generic contract() with index arrays, geometry per
+// point): 1 M DoF Q3 CG on 8 cores 0.0093 -> see docs/PARITY.md.
 template <typename T, int ND, int NQ>
-void stiffness_cell(const BdxLattice& lat, const Tables<T>& tb, const T* xv,
-                    T kappa, const T* kc, const T* u, T* y, int64_t cx, int64_t cy,
-                    int64_t cz) {
-  if (kc) kappa = kc[(cx * lat.n[1] + cy) * lat.n[2] + cz];  // per-cell coefficient
-  constexpr int nd3 = ND * ND * ND, nq3 = NQ * NQ * NQ;
+struct CellTables {
+  T B[NQ][ND], D[NQ][NQ], w[NQ], q[NQ];
+  bool ident;
+  explicit CellTables(const Tables<T>& tb) : ident(tb.identity) {
+    for (int a = 0; a < NQ; ++a) {
+      for (int i = 0; i < ND; ++i) B[a][i] = tb.phi0[a * ND + i];
+      for (int m = 0; m < NQ; ++m) D[a][m] = tb.dphi1[a * NQ + m];
+      w[a] = tb.wts[a];
+      q[a] = tb.qpts[a];
+    }
+  }
+};
+
+template <typename T, int ND, int NQ>
+void stiffness_cell_fast(const BdxLattice& lat, const CellTables<T, ND, NQ>& tb, const T* xv,
+                         const T* Gc, T kappa, const T* kc, const T* u, T* y, int64_t cx,
+                         int64_t cy, int64_t cz) {
+  if (kc) kappa = kc[(cx * lat.n[1] + cy) * lat.n[2] + cz];
+  constexpr int nd3 = ND * ND * ND, NQ2 = NQ * NQ, nq3 = NQ * NQ2;
   const int64_t P = lat.P;
-  T ue[nd3];
+  T ue[ND][ND][ND];
   int64_t dof[nd3];
   bool bc[nd3];
   for (int i = 0; i < ND; ++i)
@@ -168,45 +190,155 @@ void stiffness_cell(const BdxLattice& lat, const Tables<T>& tb, const T* xv,
         const int64_t li = cx * P + i, lj = cy * P + j, lk = cz * P + k;
         dof[a] = lat.idx(li, lj, lk);
         bc[a] = lat.is_bc(li, lj, lk);
-        ue[a] = bc[a] ? T(0) : u[dof[a]];
+        ue[i][j][k] = bc[a] ? T(0) : u[dof[a]];
       }
-  T U[nq3], t1[nq3], t2[nq3];
-  interp<T, ND, NQ>(tb, ue, U, t1, t2);
+  // interpolation to the quadrature points (z, y, x)
+  T U[NQ][NQ][NQ];
+  if (tb.ident && ND == NQ) {
+    std::memcpy(U, ue, sizeof(T) * nq3);
+  } else {
+    T t1[ND][ND][NQ], t2[ND][NQ][NQ];
+    for (int i = 0; i < ND; ++i)
+      for (int j = 0; j < ND; ++j)
+        for (int qz = 0; qz < NQ; ++qz) {
+          T s = 0;
+          for (int k = 0; k < ND; ++k) s += tb.B[qz][k] * ue[i][j][k];
+          t1[i][j][qz] = s;
+        }
+    for (int i = 0; i < ND; ++i)
+      for (int qy = 0; qy < NQ; ++qy) {
+        T acc[NQ] = {};
+        for (int j = 0; j < ND; ++j)
+          for (int qz = 0; qz < NQ; ++qz) acc[qz] += tb.B[qy][j] * t1[i][j][qz];
+        for (int qz = 0; qz < NQ; ++qz) t2[i][qy][qz] = acc[qz];
+      }
+    for (int qx = 0; qx < NQ; ++qx) {
+      T acc[NQ2] = {};
+      for (int i = 0; i < ND; ++i)
+        for (int p = 0; p < NQ2; ++p) acc[p] += tb.B[qx][i] * (&t2[i][0][0])[p];
+      std::memcpy(&U[qx][0][0], acc, sizeof(acc));
+    }
+  }
+  // reference gradient
+  T gx[NQ][NQ][NQ], gy[NQ][NQ][NQ], gz[NQ][NQ][NQ];
+  for (int qx = 0; qx < NQ; ++qx) {
+    T acc[NQ2] = {};
+    for (int m = 0; m < NQ; ++m)
+      for (int p = 0; p < NQ2; ++p) acc[p] += tb.D[qx][m] * (&U[m][0][0])[p];
+    std::memcpy(&gx[qx][0][0], acc, sizeof(acc));
+  }
+  for (int qx = 0; qx < NQ; ++qx)
+    for (int qy = 0; qy < NQ; ++qy) {
+      T acc[NQ] = {};
+      for (int m = 0; m < NQ; ++m)
+        for (int qz = 0; qz < NQ; ++qz) acc[qz] += tb.D[qy][m] * U[qx][m][qz];
+      for (int qz = 0; qz < NQ; ++qz) gy[qx][qy][qz] = acc[qz];
+      for (int qz = 0; qz < NQ; ++qz) {
+        T s = 0;
+        for (int m = 0; m < NQ; ++m) s += tb.D[qz][m] * U[qx][qy][m];
+        gz[qx][qy][qz] = s;
+      }
+    }
+  // kappa G grad u
   T X[8][3];
-  cell_vertices(lat, xv, cx, cy, cz, X);
-  const int eq[3] = {NQ, NQ, NQ};
-  T gx[nq3], gy[nq3], gz[nq3];
-  contract(tb.dphi1, NQ, NQ, false, U, eq, 0, gx);
-  contract(tb.dphi1, NQ, NQ, false, U, eq, 1, gy);
-  contract(tb.dphi1, NQ, NQ, false, U, eq, 2, gz);
+  if (!Gc) cell_vertices(lat, xv, cx, cy, cz, X);
   for (int qx = 0; qx < NQ; ++qx)
     for (int qy = 0; qy < NQ; ++qy)
       for (int qz = 0; qz < NQ; ++qz) {
         const int q = (qx * NQ + qy) * NQ + qz;
         T G[6];
-        const T w = tb.wts[qx] * tb.wts[qy] * tb.wts[qz];
-        geometry_point<T>(X, tb.qpts[qx], tb.qpts[qy], tb.qpts[qz], w, G);
-        const T a = gx[q], b = gy[q], c = gz[q];
-        gx[q] = kappa * (G[0] * a + G[1] * b + G[2] * c);
-        gy[q] = kappa * (G[1] * a + G[3] * b + G[4] * c);
-        gz[q] = kappa * (G[2] * a + G[4] * b + G[5] * c);
+        if (Gc) {
+          for (int c = 0; c < 6; ++c) G[c] = Gc[c * nq3 + q];
+        } else {
+          geometry_point<T>(X, tb.q[qx], tb.q[qy], tb.q[qz], tb.w[qx] * tb.w[qy] * tb.w[qz], G);
+        }
+        const T a = gx[qx][qy][qz], b = gy[qx][qy][qz], c = gz[qx][qy][qz];
+        gx[qx][qy][qz] = kappa * (G[0] * a + G[1] * b + G[2] * c);
+        gy[qx][qy][qz] = kappa * (G[1] * a + G[3] * b + G[4] * c);
+        gz[qx][qy][qz] = kappa * (G[2] * a + G[4] * b + G[5] * c);
       }
-  T r[nq3];
-  contract(tb.dphi1, NQ, NQ, true, gx, eq, 0, r);
-  contract(tb.dphi1, NQ, NQ, true, gy, eq, 1, t1);
-  for (int q = 0; q < nq3; ++q) r[q] += t1[q];
-  contract(tb.dphi1, NQ, NQ, true, gz, eq, 2, t1);
-  for (int q = 0; q < nq3; ++q) r[q] += t1[q];
-  T ye[nd3];
-  interp_t<T, ND, NQ>(tb, r, ye, t1, t2);
+  // transposed gradient: r = Dx^T gx + Dy^T gy + Dz^T gz
+  T r[NQ][NQ][NQ];
+  for (int m = 0; m < NQ; ++m) {
+    T acc[NQ2] = {};
+    for (int qx = 0; qx < NQ; ++qx)
+      for (int p = 0; p < NQ2; ++p) acc[p] += tb.D[qx][m] * (&gx[qx][0][0])[p];
+    std::memcpy(&r[m][0][0], acc, sizeof(acc));
+  }
+  for (int qx = 0; qx < NQ; ++qx)
+    for (int m = 0; m < NQ; ++m) {
+      T acc[NQ] = {};
+      for (int qy = 0; qy < NQ; ++qy)
+        for (int qz = 0; qz < NQ; ++qz) acc[qz] += tb.D[qy][m] * gy[qx][qy][qz];
+      for (int qz = 0; qz < NQ; ++qz) r[qx][m][qz] += acc[qz];
+    }
+  for (int qx = 0; qx < NQ; ++qx)
+    for (int qy = 0; qy < NQ; ++qy) {
+      T acc[NQ] = {};
+      for (int qz = 0; qz < NQ; ++qz)
+        for (int m = 0; m < NQ; ++m) acc[m] += tb.D[qz][m] * gz[qx][qy][qz];
+      for (int m = 0; m < NQ; ++m) r[qx][qy][m] += acc[m];
+    }
+  // transposed interpolation (x, y, z)
+  T ye[ND][ND][ND];
+  if (tb.ident && ND == NQ) {
+    std::memcpy(ye, r, sizeof(T) * nd3);
+  } else {
+    T t2[ND][NQ][NQ], t1[ND][ND][NQ];
+    for (int i = 0; i < ND; ++i) {
+      T acc[NQ2] = {};
+      for (int qx = 0; qx < NQ; ++qx)
+        for (int p = 0; p < NQ2; ++p) acc[p] += tb.B[qx][i] * (&r[qx][0][0])[p];
+      std::memcpy(&t2[i][0][0], acc, sizeof(acc));
+    }
+    for (int i = 0; i < ND; ++i)
+      for (int j = 0; j < ND; ++j) {
+        T acc[NQ] = {};
+        for (int qy = 0; qy < NQ; ++qy)
+          for (int qz = 0; qz < NQ; ++qz) acc[qz] += tb.B[qy][j] * t2[i][qy][qz];
+        for (int qz = 0; qz < NQ; ++qz) t1[i][j][qz] = acc[qz];
+      }
+    for (int i = 0; i < ND; ++i)
+      for (int j = 0; j < ND; ++j)
+        for (int k = 0; k < ND; ++k) {
+          T s = 0;
+          for (int qz = 0; qz < NQ; ++qz) s += tb.B[qz][k] * t1[i][j][qz];
+          ye[i][j][k] = s;
+        }
+  }
+  const T* yf = &ye[0][0][0];
   for (int a = 0; a < nd3; ++a) {
     if (!bc[a]) {
-      y[dof[a]] += ye[a];
+      y[dof[a]] += yf[a];
     } else {
       const int i = a / (ND * ND), j = (a / ND) % ND, k = a % ND;
       if (lat.is_owned(cx * P + i, cy * P + j, cz * P + k)) y[dof[a]] = u[dof[a]];
     }
   }
+}
+
+// Geometry factors of every local cell in the reference layout
+// G[c][6][nq^3], c = (cx n1 + cy) n2 + cz (geometry_computation_cpu,
+// src/geometry_cpu.hpp:25-112, with 64-bit offsets: quirk Q6).
+template <typename T, int NQ>
+void geometry_all(const BdxLattice& lat, const T* wts, const T* qpts, const T* xv, T* G) {
+  constexpr int nq3 = NQ * NQ * NQ;
+#pragma omp parallel for collapse(3) schedule(static)
+  for (int64_t cx = 0; cx < lat.n[0]; ++cx)
+    for (int64_t cy = 0; cy < lat.n[1]; ++cy)
+      for (int64_t cz = 0; cz < lat.n[2]; ++cz) {
+        T X[8][3];
+        cell_vertices(lat, xv, cx, cy, cz, X);
+        T* Gc = G + ((cx * lat.n[1] + cy) * lat.n[2] + cz) * int64_t{6} * nq3;
+        for (int qx = 0; qx < NQ; ++qx)
+          for (int qy = 0; qy < NQ; ++qy)
+            for (int qz = 0; qz < NQ; ++qz) {
+              const int q = (qx * NQ + qy) * NQ + qz;
+              T g[6];
+              geometry_point<T>(X, qpts[qx], qpts[qy], qpts[qz], wts[qx] * wts[qy] * wts[qz], g);
+              for (int c = 0; c < 6; ++c) Gc[c * nq3 + q] = g[c];
+            }
+      }
 }
 
 // b += M_cell f (no BC handling; the caller zeroes BC rows afterwards).
@@ -290,6 +422,7 @@ struct StiffArgs {
   const T* u;
   T* y;
   int64_t lo[3], hi[3];
+  const T* G = nullptr;  // precomputed geometry factors (bdx_cpu_geometry) or null
 };
 
 template <typename T>
@@ -297,11 +430,29 @@ struct Stiff {
   template <int ND, int NQ>
   struct K {
     static void run(const StiffArgs<T>& a) {
+      const CellTables<T, ND, NQ> tb(a.tb);
+      constexpr int64_t gsz = 6 * NQ * NQ * NQ;
       for_cells(a.lo, a.hi, [&](int64_t cx, int64_t cy, int64_t cz) {
-        stiffness_cell<T, ND, NQ>(a.lat, a.tb, a.xv, a.kappa, a.kc, a.u, a.y, cx,
-                                  cy, cz);
+        const T* Gc = a.G ? a.G + ((cx * a.lat.n[1] + cy) * a.lat.n[2] + cz) * gsz : nullptr;
+        stiffness_cell_fast<T, ND, NQ>(a.lat, tb, a.xv, Gc, a.kappa, a.kc, a.u, a.y, cx, cy,
+                                       cz);
       });
     }
+  };
+};
+
+template <typename T>
+struct GeomArgs {
+  BdxLattice lat;
+  const T *wts, *qpts, *xv;
+  T* G;
+};
+
+template <typename T>
+struct Geom {
+  template <int ND, int NQ>
+  struct K {
+    static void run(const GeomArgs<T>& a) { geometry_all<T, NQ>(a.lat, a.wts, a.qpts, a.xv, a.G); }
   };
 };
 
@@ -490,6 +641,34 @@ int bdx_host_version() { return 1; }
       a.hi[d] = hi[d];                                                        \
     }                                                                         \
     dispatch<Stiff<T>::template K>(static_cast<int>(a.lat.P), nq, a);         \
+  }                                                                           \
+  /* the same with precomputed geometry factors G (null: on the fly) */       \
+  void bdx_cpu_stiffness_g_##SUF(const int64_t* latd, int nq, const T* phi0,  \
+                                 const T* dphi1, const T* wts, const T* qpts, \
+                                 const T* nodes, int identity, const T* xv,   \
+                                 const T* G, T kappa, const T* kc,            \
+                                 const T* u, T* y, const int64_t* lo,         \
+                                 const int64_t* hi) {                         \
+    StiffArgs<T> a;                                                           \
+    a.lat = BdxLattice::from(latd);                                           \
+    a.tb = make_tables<T>(phi0, dphi1, wts, qpts, nodes, identity);           \
+    a.xv = xv;                                                                \
+    a.G = G;                                                                  \
+    a.kappa = kappa;                                                          \
+    a.kc = kc;                                                                \
+    a.u = u;                                                                  \
+    a.y = y;                                                                  \
+    for (int d = 0; d < 3; ++d) {                                             \
+      a.lo[d] = lo[d];                                                        \
+      a.hi[d] = hi[d];                                                        \
+    }                                                                         \
+    dispatch<Stiff<T>::template K>(static_cast<int>(a.lat.P), nq, a);         \
+  }                                                                           \
+  /* geometry factors of every local cell, reference layout [c][6][nq^3] */  \
+  void bdx_cpu_geometry_##SUF(const int64_t* latd, int nq, const T* wts,      \
+                              const T* qpts, const T* xv, T* G) {             \
+    GeomArgs<T> a{BdxLattice::from(latd), wts, qpts, xv, G};                  \
+    dispatch<Geom<T>::template K>(static_cast<int>(a.lat.P), nq, a);          \
   }                                                                           \
   void bdx_cpu_mass_##SUF(const int64_t* latd, int nq, const T* phi0,         \
                           const T* dphi1, const T* wts, const T* qpts,        \

@@ -243,11 +243,30 @@ class PoissonProblem:
 class MatFreeLaplacianCPU:
     """CPU operator (C++/OpenMP, both qmodes; src/laplacian.hpp:450-771)."""
 
+    # geometry factors precomputed per cell (reference layout [c][6][nq^3],
+    # src/laplacian.hpp:515-541) when they fit in this many bytes, else
+    # computed per point on the fly.  Default 0 (on the fly): on this 8-core
+    # host the stored-G apply is memory-bound and slower at 8 threads (73 vs
+    # 49 ms per 1 M DoF Q3 apply; faster on one thread, 182 vs 365 ms).
+    # BDX_CPU_G_MAX_BYTES overrides.
+    G_MAX_BYTES = 0
+
     def __init__(self, problem: PoissonProblem):
+        import os
         self.pb = problem
         self.lib = native.host()
-        self._fn = getattr(self.lib, f"bdx_cpu_stiffness_{problem.suf}")
+        self._fn = getattr(self.lib, f"bdx_cpu_stiffness_g_{problem.suf}")
         self.latd = problem.lat.as_int64()
+        nq = problem.tables.nq
+        ncells = int(np.prod(problem.lat.n))
+        nbytes = ncells * 6 * nq ** 3 * problem.new_vector().element_size()
+        self.G = None
+        if nbytes <= int(os.environ.get("BDX_CPU_G_MAX_BYTES", self.G_MAX_BYTES)):
+            t = problem.host_tables
+            self.G = np.empty(ncells * 6 * nq ** 3, dtype=t["wts"].dtype)
+            getattr(self.lib, f"bdx_cpu_geometry_{problem.suf}")(
+                ptr(self.latd), nq, ptr(t["wts"]), ptr(t["qpts"]), ptr(problem.xv_host),
+                ptr(self.G))
 
     def _cells(self, u, y, lo, hi):
         t = self.pb.host_tables
@@ -255,7 +274,8 @@ class MatFreeLaplacianCPU:
         hi = np.asarray(hi, dtype=np.int64)
         self._fn(ptr(self.latd), self.pb.tables.nq, ptr(t["phi0"]), ptr(t["dphi1"]),
                  ptr(t["wts"]), ptr(t["qpts"]), ptr(t["nodes"]),
-                 int(self.pb.tables.is_identity), ptr(self.pb.xv_host), self.pb.kappa,
+                 int(self.pb.tables.is_identity), ptr(self.pb.xv_host),
+                 ptr(self.G) if self.G is not None else None, self.pb.kappa,
                  ptr(self.pb.kc_host), ptr(u.numpy()), ptr(y.numpy()), ptr(lo), ptr(hi))
 
     def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:

@@ -65,6 +65,9 @@ def host():
             for suf, ft in (("f64", f64), ("f32", f32)):
                 _declare(lib, f"bdx_cpu_stiffness_{suf}",
                          [vp, i32, vp, vp, vp, vp, vp, i32, vp, ft, vp, vp, vp, vp, vp])
+                _declare(lib, f"bdx_cpu_stiffness_g_{suf}",
+                         [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, ft, vp, vp, vp, vp, vp])
+                _declare(lib, f"bdx_cpu_geometry_{suf}", [vp, i32, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_mass_{suf}",
                          [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_csr_{suf}",
