@@ -136,7 +136,7 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
     mark("operator")
     # one operator action on the RHS before the CG (untimed): the
     # cross-family consistency check of _record compares these scalars
-    check = _action_check(pb, op, u) if gpu else None
+    check = _action_check(pb, op, u)
 
     def sync():
         if gpu:
@@ -283,13 +283,15 @@ def _action_check(pb, op, u) -> dict:
     import torch
     z = pb.new_vector()
     op.apply(u, z)
-    torch.cuda.synchronize()
+    if z.is_cuda:
+        torch.cuda.synchronize()
     w = 1.0 + 0.5 * torch.sin(torch.arange(z.numel(), dtype=torch.float64, device=z.device) * 0.7
                               + 0.3)
     w = w.view(z.shape) * z.double()
     out = {"norm": pb.norm(z), "wdot": pb.inner(z, w)}
     del z, w
-    torch.cuda.empty_cache()
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
     return out
 
 
@@ -454,12 +456,13 @@ def run(comm, a) -> dict | None:
             except Exception as e:
                 raise MeasurementFailed(f"{key}: {e!r}", (head, companions, {})) from e
     extras = {}
-    if gpu and a.extras == "auto" and n > 1 and a.config == "q3" and not a.mesh:
+    if a.extras == "auto" and n > 1 and a.config == "q3" and not a.mesh:
         # N > 1: the reference's own data model (dofmap + stored G, the
         # layout of its published 64-rank runs, /root/reference/src/
         # laplacian.hpp:281-349) on this weak-scaled mesh, in-process after
         # the companions, at the headline's steps / warm-up, with its per-rank
-        # split-schedule timeline
+        # split-schedule timeline; on the CPU platform
+        # the same record comes from the C++ dofmap operator (DofmapLaplacianCPU)
         try:
             extras["dofmap"] = _guarded(comm, lambda: _measure(
                 comm, a, a.config, a.steps, a.warmup, kappa=a.kappa, perturb=a.perturb,

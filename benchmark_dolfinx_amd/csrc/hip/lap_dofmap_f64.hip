@@ -7,6 +7,7 @@ BDX_DOFMAP_API(double, f64)
 // kernel choice of the FP64 dofmap launches (lap_dofmap.h): -1 = environment
 // (BDX_DOFMAP_MFMA) / default, 0 = VALU kernel, 1 = MFMA kernel
 static int g_dofmap_mfma = -1;
+// Select the FP64 dofmap operator kernel for later launches (tests, A/B).
 extern "C" int bdx_dofmap_set_mfma(int mode) {
   g_dofmap_mfma = mode < 0 ? -1 : (mode ? 1 : 0);
   return 0;

@@ -173,25 +173,13 @@ struct CellTables {
   }
 };
 
+// ye = A_e ue for one cell (no BC handling): geometry factors from Gc
+// (reference layout [6][nq^3]) or, when Gc is null, per point from the
+// cell's vertices X.
 template <typename T, int ND, int NQ>
-void stiffness_cell_fast(const BdxLattice& lat, const CellTables<T, ND, NQ>& tb, const T* xv,
-                         const T* Gc, T kappa, const T* kc, const T* u, T* y, int64_t cx,
-                         int64_t cy, int64_t cz) {
-  if (kc) kappa = kc[(cx * lat.n[1] + cy) * lat.n[2] + cz];
+inline void cell_core(const CellTables<T, ND, NQ>& tb, const T (&ue)[ND][ND][ND], const T* Gc,
+                      const T (*X)[3], T kappa, T (&ye)[ND][ND][ND]) {
   constexpr int nd3 = ND * ND * ND, NQ2 = NQ * NQ, nq3 = NQ * NQ2;
-  const int64_t P = lat.P;
-  T ue[ND][ND][ND];
-  int64_t dof[nd3];
-  bool bc[nd3];
-  for (int i = 0; i < ND; ++i)
-    for (int j = 0; j < ND; ++j)
-      for (int k = 0; k < ND; ++k) {
-        const int a = (i * ND + j) * ND + k;
-        const int64_t li = cx * P + i, lj = cy * P + j, lk = cz * P + k;
-        dof[a] = lat.idx(li, lj, lk);
-        bc[a] = lat.is_bc(li, lj, lk);
-        ue[i][j][k] = bc[a] ? T(0) : u[dof[a]];
-      }
   // interpolation to the quadrature points (z, y, x)
   T U[NQ][NQ][NQ];
   if (tb.ident && ND == NQ) {
@@ -240,8 +228,6 @@ void stiffness_cell_fast(const BdxLattice& lat, const CellTables<T, ND, NQ>& tb,
       }
     }
   // kappa G grad u
-  T X[8][3];
-  if (!Gc) cell_vertices(lat, xv, cx, cy, cz, X);
   for (int qx = 0; qx < NQ; ++qx)
     for (int qy = 0; qy < NQ; ++qy)
       for (int qz = 0; qz < NQ; ++qz) {
@@ -280,7 +266,6 @@ void stiffness_cell_fast(const BdxLattice& lat, const CellTables<T, ND, NQ>& tb,
       for (int m = 0; m < NQ; ++m) r[qx][qy][m] += acc[m];
     }
   // transposed interpolation (x, y, z)
-  T ye[ND][ND][ND];
   if (tb.ident && ND == NQ) {
     std::memcpy(ye, r, sizeof(T) * nd3);
   } else {
@@ -306,6 +291,31 @@ void stiffness_cell_fast(const BdxLattice& lat, const CellTables<T, ND, NQ>& tb,
           ye[i][j][k] = s;
         }
   }
+}
+
+template <typename T, int ND, int NQ>
+void stiffness_cell_fast(const BdxLattice& lat, const CellTables<T, ND, NQ>& tb, const T* xv,
+                         const T* Gc, T kappa, const T* kc, const T* u, T* y, int64_t cx,
+                         int64_t cy, int64_t cz) {
+  if (kc) kappa = kc[(cx * lat.n[1] + cy) * lat.n[2] + cz];
+  constexpr int nd3 = ND * ND * ND;
+  const int64_t P = lat.P;
+  T ue[ND][ND][ND];
+  int64_t dof[nd3];
+  bool bc[nd3];
+  for (int i = 0; i < ND; ++i)
+    for (int j = 0; j < ND; ++j)
+      for (int k = 0; k < ND; ++k) {
+        const int a = (i * ND + j) * ND + k;
+        const int64_t li = cx * P + i, lj = cy * P + j, lk = cz * P + k;
+        dof[a] = lat.idx(li, lj, lk);
+        bc[a] = lat.is_bc(li, lj, lk);
+        ue[i][j][k] = bc[a] ? T(0) : u[dof[a]];
+      }
+  T X[8][3];
+  if (!Gc) cell_vertices(lat, xv, cx, cy, cz, X);
+  T ye[ND][ND][ND];
+  cell_core<T, ND, NQ>(tb, ue, Gc, X, kappa, ye);
   const T* yf = &ye[0][0][0];
   for (int a = 0; a < nd3; ++a) {
     if (!bc[a]) {
@@ -316,6 +326,115 @@ void stiffness_cell_fast(const BdxLattice& lat, const CellTables<T, ND, NQ>& tb,
     }
   }
 }
+
+// The reference data model on the CPU (its MatFreeLaplacianCPU gathers
+// through the cell -> dof map with G stored per cell, src/laplacian.hpp:
+// 592-631): y += A u over the listed cells, cell_dofs (sign bit = writer,
+// ignored here), per-dof flags (bit 0 Dirichlet, bit 1 owned), stored G
+// [cell][6][nq^3] or per-point geometry from cell_verts / coords.  Cells run
+// in parallel; the scatter uses atomic adds (any mesh, any cell order), the
+// Dirichlet identity rows an atomic write of u (every writer writes the
+// same value).
+template <typename T, int ND, int NQ>
+void dofmap_cells(const CellTables<T, ND, NQ>& tb, const int* cells, int ncl, const int* cdofs,
+                  const int* cverts, const T* coords, const T* G,
+                  const unsigned char* flags, T kappa, const T* kc, const T* u, T* y) {
+  constexpr int nd3 = ND * ND * ND, nq3 = NQ * NQ * NQ;
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int li = 0; li < ncl; ++li) {
+    const int64_t c = cells[li];
+    T ue[ND][ND][ND];
+    T* uf = &ue[0][0][0];
+    int64_t dof[nd3];
+    unsigned char fl[nd3];
+    for (int a = 0; a < nd3; ++a) {
+      dof[a] = cdofs[c * nd3 + a] & 0x7fffffff;
+      fl[a] = flags[dof[a]];
+      uf[a] = (fl[a] & 1u) ? T(0) : u[dof[a]];
+    }
+    T X[8][3];
+    if (!G)
+      for (int v = 0; v < 8; ++v)
+        for (int d = 0; d < 3; ++d) X[v][d] = coords[3 * int64_t{cverts[c * 8 + v]} + d];
+    T ye[ND][ND][ND];
+    cell_core<T, ND, NQ>(tb, ue, G ? G + c * 6 * nq3 : nullptr, X, kc ? kc[c] : kappa, ye);
+    const T* yf = &ye[0][0][0];
+    for (int a = 0; a < nd3; ++a) {
+      if (!(fl[a] & 1u)) {
+#pragma omp atomic
+        y[dof[a]] += yf[a];
+      } else if (fl[a] & 2u) {
+#pragma omp atomic write
+        y[dof[a]] = u[dof[a]];
+      }
+    }
+  }
+}
+
+template <typename T>
+struct DofArgsCPU {
+  Tables<T> tb;
+  const int *cells, *cdofs, *cverts;
+  int ncl;
+  const T *coords, *G;
+  const unsigned char* flags;
+  T kappa;
+  const T *kc, *u;
+  T* y;
+};
+
+template <typename T>
+struct DofmapCPU {
+  template <int ND, int NQ>
+  struct K {
+    static void run(const DofArgsCPU<T>& a) {
+      const CellTables<T, ND, NQ> tb(a.tb);
+      dofmap_cells<T, ND, NQ>(tb, a.cells, a.ncl, a.cdofs, a.cverts, a.coords, a.G, a.flags,
+                              a.kappa, a.kc, a.u, a.y);
+    }
+  };
+};
+
+// Stored G of explicit cells (cell_verts / coords): the reference's
+// geometry_computation_cpu on the dofmap data model.
+template <typename T, int NQ>
+void dofmap_geometry_cpu(int ncells, const int* cverts, const T* coords, const T* wts,
+                         const T* qpts, T* G) {
+  constexpr int nq3 = NQ * NQ * NQ;
+#pragma omp parallel for schedule(static)
+  for (int c = 0; c < ncells; ++c) {
+    T X[8][3];
+    for (int v = 0; v < 8; ++v)
+      for (int d = 0; d < 3; ++d) X[v][d] = coords[3 * int64_t{cverts[int64_t{c} * 8 + v]} + d];
+    T* Gc = G + int64_t{c} * 6 * nq3;
+    for (int qx = 0; qx < NQ; ++qx)
+      for (int qy = 0; qy < NQ; ++qy)
+        for (int qz = 0; qz < NQ; ++qz) {
+          const int q = (qx * NQ + qy) * NQ + qz;
+          T g[6];
+          geometry_point<T>(X, qpts[qx], qpts[qy], qpts[qz], wts[qx] * wts[qy] * wts[qz], g);
+          for (int k = 0; k < 6; ++k) Gc[k * nq3 + q] = g[k];
+        }
+  }
+}
+
+template <typename T>
+struct DofGeomArgs {
+  int ncells;
+  const int* cverts;
+  const T *coords, *wts, *qpts;
+  T* G;
+};
+
+template <typename T>
+struct DofGeomCPU {
+  template <int ND, int NQ>
+  struct K {
+    static void run(const DofGeomArgs<T>& a) {
+      dofmap_geometry_cpu<T, NQ>(a.ncells, a.cverts, a.coords, a.wts, a.qpts, a.G);
+    }
+  };
+};
 
 // Geometry factors of every local cell in the reference layout
 // G[c][6][nq^3], c = (cx n1 + cy) n2 + cz (geometry_computation_cpu,
@@ -663,6 +782,25 @@ int bdx_host_version() { return 1; }
       a.hi[d] = hi[d];                                                        \
     }                                                                         \
     dispatch<Stiff<T>::template K>(static_cast<int>(a.lat.P), nq, a);         \
+  }                                                                           \
+  /* the reference data model on the CPU (dofmap_cells) */                   \
+  void bdx_cpu_dofmap_##SUF(int P, int nq, const T* phi0, const T* dphi1,     \
+                            const T* wts, const T* qpts, int identity,        \
+                            const int* cells, int ncl, const int* cdofs,      \
+                            const int* cverts, const T* coords, const T* G,   \
+                            const unsigned char* flags, T kappa, const T* kc, \
+                            const T* u, T* y) {                               \
+    DofArgsCPU<T> a{make_tables<T>(phi0, dphi1, wts, qpts, nullptr, identity), \
+                    cells, cdofs, cverts, ncl, coords, G, flags, kappa, kc,  \
+                    u, y};                                                    \
+    dispatch<DofmapCPU<T>::template K>(P, nq, a);                             \
+  }                                                                           \
+  void bdx_cpu_dofmap_geometry_##SUF(int P, int nq, const T* wts,             \
+                                     const T* qpts, int ncells,               \
+                                     const int* cverts, const T* coords,      \
+                                     T* G) {                                  \
+    DofGeomArgs<T> a{ncells, cverts, coords, wts, qpts, G};                   \
+    dispatch<DofGeomCPU<T>::template K>(P, nq, a);                            \
   }                                                                           \
   /* geometry factors of every local cell, reference layout [c][6][nq^3] */  \
   void bdx_cpu_geometry_##SUF(const int64_t* latd, int nq, const T* wts,      \

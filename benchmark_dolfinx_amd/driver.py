@@ -34,6 +34,10 @@ class BenchmarkResults:
 
 def make_operator(pb: PoissonProblem, kernel: str = "auto", geometry: str = "auto"):
     if pb.platform == "cpu":
+        if kernel == "dofmap":
+            # the reference's own CPU data model (cell -> dof map, stored G)
+            from .models.unstructured import DofmapLaplacianCPU
+            return DofmapLaplacianCPU(pb, "otf" if geometry == "otf" else "stored")
         return MatFreeLaplacianCPU(pb)
     if kernel == "auto":
         # measured on MI355X (profiles/): fused3 wins on parallelepiped meshes

@@ -277,3 +277,67 @@ class DofmapLaplacianGPU:
         plast = self.p_b if (cg.it - 1) % 2 == 0 else self.p_a
         self.k.dofmap_xflush(cg.x.view(-1), plast, cg.scal, last, self.PAP)
         self.x_lag = False
+
+
+class DofmapLaplacianCPU:
+    """The reference data model on the CPU platform: the C++/OpenMP operator
+    gathers through the explicit cell -> dof map with G stored per cell in the
+    reference layout [cell][6][nq^3] (the reference's MatFreeLaplacianCPU with
+    geometry_computation_cpu, src/laplacian.hpp:450-771,
+    src/geometry_cpu.hpp:25-112; 64-bit offsets, quirk Q6), scatters with
+    atomic adds and runs the same interior / boundary split around the
+    forward halo exchange as the GPU operator.  geometry="otf": per-point
+    geometry from the cell vertices instead of stored G."""
+
+    name = "dofmap"
+
+    def __init__(self, problem, geometry: str = "stored", mesh: UnstructuredMesh | None = None):
+        from ..ops import native
+        if problem.platform != "cpu":
+            raise ValueError("DofmapLaplacianCPU runs on the CPU platform")
+        if geometry not in ("otf", "stored"):
+            raise ValueError(f"unknown geometry mode {geometry}")
+        self.pb = problem
+        self.geometry = f"dofmap-{geometry}"
+        self.lib = native.host()
+        suf = problem.suf
+        self._fn = getattr(self.lib, f"bdx_cpu_dofmap_{suf}")
+        npdt = np.float64 if suf == "f64" else np.float32
+        with timed("~setup dofmap"):
+            self.mesh = m = mesh or UnstructuredMesh.from_problem(problem)
+            self.cdofs = np.ascontiguousarray(m.cell_dofs, dtype=np.int32)
+            self.cverts = np.ascontiguousarray(m.cell_verts, dtype=np.int32)
+            self.coords = np.ascontiguousarray(m.coords, dtype=npdt)
+            self.flags = np.ascontiguousarray(m.dof_flags, dtype=np.uint8)
+            self.inner = np.ascontiguousarray(m.interior_cells, dtype=np.int32)
+            self.outer = np.ascontiguousarray(m.boundary_cells, dtype=np.int32)
+            self.kc = None if m.kc is None else np.ascontiguousarray(m.kc, dtype=npdt)
+            t = problem.host_tables
+            self.t = t
+            self.G = None
+            if geometry == "stored":
+                nq = problem.tables.nq
+                self.G = np.empty(m.ncells * 6 * nq ** 3, dtype=npdt)
+                getattr(self.lib, f"bdx_cpu_dofmap_geometry_{suf}")(
+                    problem.lat.degree, nq, native.ptr(t["wts"]), native.ptr(t["qpts"]),
+                    m.ncells, native.ptr(self.cverts), native.ptr(self.coords),
+                    native.ptr(self.G))
+
+    def _run(self, cells, u, y):
+        from ..ops.native import ptr
+        if cells.size == 0:
+            return
+        t, pb = self.t, self.pb
+        self._fn(pb.lat.degree, pb.tables.nq, ptr(t["phi0"]), ptr(t["dphi1"]), ptr(t["wts"]),
+                 ptr(t["qpts"]), int(pb.tables.is_identity), ptr(cells), int(cells.size),
+                 ptr(self.cdofs), ptr(self.cverts), ptr(self.coords), ptr(self.G), ptr(self.flags),
+                 pb.kappa, ptr(self.kc), ptr(u), ptr(y))
+
+    def apply(self, u: torch.Tensor, y: torch.Tensor) -> None:
+        pb = self.pb
+        y.zero_()
+        work = pb.halo.forward_begin(u)
+        self._run(self.inner, u, y)      # overlaps the forward exchange
+        pb.halo.forward_end(u, work)
+        self._run(self.outer, u, y)
+        pb.halo.reverse(y)

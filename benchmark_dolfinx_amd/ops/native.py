@@ -68,6 +68,10 @@ def host():
                 _declare(lib, f"bdx_cpu_stiffness_g_{suf}",
                          [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, ft, vp, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_geometry_{suf}", [vp, i32, vp, vp, vp, vp])
+                _declare(lib, f"bdx_cpu_dofmap_{suf}",
+                         [i32, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, ft, vp,
+                          vp, vp])
+                _declare(lib, f"bdx_cpu_dofmap_geometry_{suf}", [i32, i32, vp, vp, i32, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_mass_{suf}",
                          [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp])
                 _declare(lib, f"bdx_cpu_csr_{suf}",

@@ -121,3 +121,29 @@ def test_world_size_mismatch_is_refused():
                        cwd=ROOT, env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"),
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_multirank_run_records_the_reference_data_model():
+    """N > 1: after the headline and companions, rank 0's
+    record carries the reference data model (dofmap + stored G) on the same
+    weak-scaled mesh, timed with the headline's steps / warm-up, and the
+    cross-family consistency pair q3~dofmap; here on 2 / 4 / 8 gloo ranks
+    with the C++ CPU dofmap operator (the GPU path is the same code with the
+    HIP kernel and RCCL, tests/test_gpu_distributed_emulated.py)."""
+    one = _line(_bench(["--gpus", "1", "--dofs-per-gpu", "24000", "--steps", "3", "--warmup",
+                        "1", "--profile-steps", "0", "--companions", "off"]))
+    assert not one["variants"]  # one CPU rank: no variants (GPU-only extras)
+    for n in (2, 4, 8):
+        rec = _line(_bench(["--gpus", str(n), "--dofs-per-gpu", str(24000 // n), "--steps", "3",
+                            "--warmup", "1", "--profile-steps", "0", "--companions", "off"],
+                           timeout=400, BDX_PARTITION="yz"))
+        dm = rec["variants"]["dofmap"]
+        assert dm.get("error") is None, dm
+        assert dm["kernel"] == "dofmap" and dm["geometry"] == "dofmap-stored"
+        assert dm["steps"] == 3 and dm["warmup"] == 1 and dm["value"] > 0
+        assert rec["dofmap_gdofs"] == dm["value"]
+        assert dm["mesh"] == rec["config"]["mesh"] == one["config"]["mesh"]
+        assert dm["comm"]["torch_world"] == n
+        pair = rec["consistency"]["pairs"]["q3~dofmap"]
+        assert pair["ok"] and pair["action_norm"] < 1e-12 and pair["y_norm"] < 1e-10, pair
+        assert abs(dm["y_norm"] - one["config"]["y_norm"]) <= 1e-10 * one["config"]["y_norm"]

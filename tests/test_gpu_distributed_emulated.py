@@ -38,6 +38,20 @@ def test_bench_run_multirank_matches_single(config, total, ranks):
     assert bs["n"] > 0 and 0 < bs["tbps_min"] <= bs["tbps_max"]
     tol = 1e-11 if config != "q6f32" else 2e-5
     assert abs(got["config"]["y_norm"] - ref["config"]["y_norm"]) <= tol * ref["config"]["y_norm"]
+    if config == "q3":
+        # N > 1: the reference data model on the same mesh, in-process after
+        # the companions, with its per-rank split-schedule timeline and the
+        # cross-family consistency pair
+        dm = got["variants"]["dofmap"]
+        assert dm.get("error") is None, dm
+        assert dm["kernel"] == "dofmap" and dm["steps"] == 6 and dm["value"] > 0
+        assert got["dofmap_gdofs"] == dm["value"]
+        ppr = dm["phases_per_rank"]
+        assert ppr is not None and len(ppr) == ranks
+        assert all(p["iteration"] > 0 and p["interior_done"] > 0 for p in ppr)
+        pair = got["consistency"]["pairs"]["q3~dofmap"]
+        assert pair["ok"] and pair["action_norm"] < 1e-12, pair
+        assert got["consistency"]["ok"]
 
 
 @pytest.mark.parametrize("geometry", ["otf-general", "stored"])
