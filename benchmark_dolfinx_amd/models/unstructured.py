@@ -171,7 +171,6 @@ class DofmapLaplacianGPU:
                 self.geom = 0
         self._cg = None
         self._rt = None
-        import os
         # native (default) at every rank count.  Its multi-rank split schedule
         # is verified with thread ranks on one GPU (tests/test_gpu_dofmap.py)
         # and shares the RCCL transport of the fused runtime; a run of it on
