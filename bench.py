@@ -30,6 +30,7 @@ checkpoint / dataset exists for this workload).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -249,6 +250,11 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
     if hasattr(op, "close"):
         op.close()
     del op, x, u, pb, rt, cg
+    # the operator / runtime / problem objects hold reference cycles: collect
+    # them now, so the next measurement (or an isolated child) gets the HBM
+    # back (without this a --kernel dofmap run held ~200 GB of stale G and
+    # vectors when its Q6 children started)
+    gc.collect()
     if gpu:
         torch.cuda.empty_cache()
     return rec
@@ -405,6 +411,7 @@ def _guarded(comm, fn, log) -> dict:
         log(f"secondary measurement failed: {e!r}")
         try:
             import torch
+            gc.collect()  # what the failed measurement left in reference cycles
             if torch.cuda.is_available():
                 torch.cuda.empty_cache()
         except Exception:  # noqa: BLE001
