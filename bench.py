@@ -206,6 +206,7 @@ def _measure(comm, a, config, steps, warmup, *, kappa="constant", perturb=0.0,
         "partition": list(pb.lat.pgrid),
         "kernel": getattr(op, "name", type(op).__name__),
         "geometry": getattr(op, "geometry", "otf"),
+        "dofmap_core": getattr(op, "core", None),
         "x_segments": getattr(op, "nseg", None),
         "kappa": kappa,
         "geom_perturb_fact": perturb,
@@ -304,7 +305,8 @@ def _action_check(pb, op, u) -> dict:
 # Pairs of records that time the same problem with different operator
 # families (headline / companion key, variant key): their action checks must
 # agree to CONSISTENCY_TOL, else the run fails.
-CONSISTENCY_PAIRS = (("q3", "dofmap"), ("q6", "q6_dofmap"), ("general", "general_trilinear"))
+CONSISTENCY_PAIRS = (("q3", "dofmap"), ("q6", "q6_dofmap"), ("general", "general_trilinear"),
+                     ("dofmap", "dofmap_mfma"), ("q6_dofmap", "q6_dofmap_mfma"))
 CONSISTENCY_TOL = 1e-9
 YNORM_TOL = 1e-4  # CG iterates: rounding drift over hundreds of iterations (see above)
 
@@ -341,12 +343,27 @@ def _consistency(head, companions, extras) -> dict:
     return out
 
 
+def _measure_env(comm, a, config, steps, warmup, *, extra_env=None, **kw) -> dict:
+    """`_measure` in this process with `extra_env` set for its duration."""
+    old = {k: os.environ.get(k) for k in (extra_env or {})}
+    os.environ.update(extra_env or {})
+    try:
+        return _measure(comm, a, config, steps, warmup, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def _measure_isolated(a, config, steps, warmup, *, kappa="constant", perturb=0.0,
-                      kernel="auto", geometry="auto", log=None) -> dict:
+                      kernel="auto", geometry="auto", extra_env=None, log=None) -> dict:
     """One-rank `_measure` in a child interpreter (this script, headline only,
-    no companions / variants); returns the child's record with its own
-    clock.  The parent has released its cached device memory, and never
-    execs: the child is a fresh process started with Popen semantics."""
+    no companions / variants; `extra_env`: added to the child's environment); returns
+    the child's record with its own clock.  The parent has released its
+    cached device memory, and never execs: the child is a fresh process
+    started with Popen semantics."""
     import subprocess
 
     argv = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--config", config,
@@ -361,6 +378,7 @@ def _measure_isolated(a, config, steps, warmup, *, kappa="constant", perturb=0.0
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
                         "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(extra_env or {})
     timeout = float(os.environ.get("BDX_BENCH_CHILD_TIMEOUT_S", "600"))
     pr = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=timeout)
     for line in pr.stderr.splitlines():
@@ -379,7 +397,8 @@ def _measure_isolated(a, config, steps, warmup, *, kappa="constant", perturb=0.0
             "ms_per_step_min": d["ms_per_step_min"], "steps": d["steps"], "warmup": d["warmup"],
             "vs_baseline": d["vs_baseline"], "dtype": d["dtype"], "dofs_per_gpu": c["dofs_per_gpu"],
             "ndofs_global": c["global_batch"], "mesh": c["mesh"], "kernel": c["kernel"],
-            "geometry": c["geometry"], "x_segments": c["x_segments"], "kappa": c["kappa"],
+            "geometry": c["geometry"], "dofmap_core": c.get("dofmap_core"),
+            "x_segments": c["x_segments"], "kappa": c["kappa"],
             "geom_perturb_fact": c["geom_perturb_fact"], "y_norm": c["y_norm"],
             "action_check": c.get("action_check"),
             "setup_s": c["setup_s"], "runtime": c["runtime"], "isolated_process": True}
@@ -499,7 +518,17 @@ def run(comm, a) -> dict | None:
                  # BASELINE configs[4] "MFMA f32 tensor contractions": fused3's
                  # FP32 x-trilinear instance, whose y / z stages run on
                  # v_mfma_f32_16x16x4_f32 (lap_fused3.h kF3MfmaF32)
-                 ("q6f32_general", "q6f32", dict(kappa=a.kappa, perturb=pert)))
+                 ("q6f32_general", "q6f32", dict(kappa=a.kappa, perturb=pert)),
+                 # the reference data model with every contraction on
+                 # v_mfma_f64_16x16x4_f64 (lap_dofmfma.h; selectable, not the
+                 # default: profiles/r6_dofmap_mfma.md), same problems as
+                 # "dofmap" / "q6_dofmap", checked against them below
+                 ("dofmap_mfma", a.config, dict(kappa=a.kappa, perturb=a.perturb,
+                                                kernel="dofmap", geometry="stored",
+                                                extra_env={"BDX_DOFMAP_MFMA": "1"})),
+                 ("q6_dofmap_mfma", "q6", dict(kappa=a.kappa, perturb=a.perturb, kernel="dofmap",
+                                               geometry="stored",
+                                               extra_env={"BDX_DOFMAP_MFMA": "1"})))
         # Each variant runs in a fresh child process on one rank: in this
         # process, after the headline and the 500 M DoF companions, the
         # variants measured up to 15 % low (dofmap Q3 11.9 vs 14.0 GDoF/s on
@@ -517,7 +546,7 @@ def run(comm, a) -> dict | None:
                     extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure_isolated(
                         a, cfg, a.steps, a.warmup, log=log, **kw), log)
                 else:
-                    extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure(
+                    extras[key] = _guarded(comm, lambda cfg=cfg, kw=kw: _measure_env(
                         comm, a, cfg, a.steps, a.warmup, log=log, **kw), log)
             except Exception as e:
                 raise MeasurementFailed(f"{key}: {e!r}", (head, companions, extras)) from e
@@ -587,6 +616,7 @@ def _record(a, n, head, companions, extras, flags, gpu) -> dict:
             "mesh": head["mesh"],
             "kernel": head["kernel"],
             "geometry": head["geometry"],
+            "dofmap_core": head.get("dofmap_core"),
             "x_segments": head["x_segments"],
             "kappa": head["kappa"],
             "geom_perturb_fact": head["geom_perturb_fact"],
@@ -616,6 +646,8 @@ def _record(a, n, head, companions, extras, flags, gpu) -> dict:
         "q6_general_gdofs": extras.get("q6_general", {}).get("value"),
         "q6_dofmap_gdofs": extras.get("q6_dofmap", {}).get("value"),
         "q6f32_general_gdofs": extras.get("q6f32_general", {}).get("value"),
+        "dofmap_mfma_gdofs": extras.get("dofmap_mfma", {}).get("value"),
+        "q6_dofmap_mfma_gdofs": extras.get("q6_dofmap_mfma", {}).get("value"),
         "variants": extras,
         "consistency": _consistency(head, companions, extras),
     }

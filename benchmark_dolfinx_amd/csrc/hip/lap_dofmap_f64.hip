@@ -18,6 +18,13 @@ int bdx_dofmap_mfma_mode() {
   if (e && *e) return std::atoi(e) ? 1 : 0;
   return -1;
 }
+// Which kernel an FP64 dofmap launch of this element takes right now (the
+// selection of launch_dofmap): 1 = lap_dofmfma_kernel, 0 = lap_dofmap_kernel.
+extern "C" int bdx_dofmap_uses_mfma(int nd, int nq) {
+  if (nd > 8 || nq > 8) return 0;
+  const int mm = bdx_dofmap_mfma_mode();
+  return (mm == 1 || (mm < 0 && kDofMfmaDefault(nq))) ? 1 : 0;
+}
 
 // Writer designation of the dofmap CG (type independent): the first
 // occurrence of every dof over the launch order [cells_a..., cells_b...]

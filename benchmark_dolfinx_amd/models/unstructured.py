@@ -169,6 +169,12 @@ class DofmapLaplacianGPU:
                 self.G = torch.empty(m.ncells * 6 * nq3, dtype=dt, device=dev)
                 self.k.dofmap_geometry(m.ncells, self.cverts, self.coords, self.G)
                 self.geom = 0
+        # the FP64 operator kernel the launches take (lap_dofmap.h: the VALU
+        # line-per-lane kernel by default, lap_dofmfma.h's MFMA one under
+        # BDX_DOFMAP_MFMA=1 / bdx_dofmap_set_mfma); FP32 is always VALU
+        nd, nq = problem.tables.nd, problem.tables.nq
+        self.core = ("mfma" if dt == torch.float64 and self.k.lib.bdx_dofmap_uses_mfma(nd, nq)
+                     else "valu")
         self._cg = None
         self._rt = None
         # native (default) at every rank count.  Its multi-rank split schedule

@@ -74,6 +74,7 @@ def declare(lib) -> None:
                                      vp], vp)
     _d(lib, "bdx_dofmap_nblocks", [i32, i32])
     _d(lib, "bdx_dofmap_set_mfma", [i32])
+    _d(lib, "bdx_dofmap_uses_mfma", [i32, i32])
     _d(lib, "bdx_rt_tiled", [vp])
     _d(lib, "bdx_rt_connect", [vp, vp, i32])
     _d(lib, "bdx_rt_comm_count", [vp])

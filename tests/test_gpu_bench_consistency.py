@@ -26,7 +26,7 @@ def _bench(**env):
     args = [sys.executable, "bench.py", "--dofs-per-gpu", "2000000", "--steps", "3", "--warmup",
             "1", "--companions", "off", "--extras", "on", "--box-probe", "off",
             "--profile-steps", "0"]
-    return subprocess.run(args, cwd=ROOT, env=e, capture_output=True, text=True, timeout=280)
+    return subprocess.run(args, cwd=ROOT, env=e, capture_output=True, text=True, timeout=420)
 
 
 def _line(r):
@@ -42,6 +42,14 @@ def test_consistency_gate_passes_and_catches_a_corrupt_dofmap_table():
     pair = rec["consistency"]["pairs"]["q3~dofmap"]
     assert pair["ok"] and pair["action_norm"] < 1e-12 and pair["action_wdot"] < 1e-12, pair
     assert rec["consistency"]["pairs"]["general~general_trilinear"]["ok"]
+    # the MFMA kernel of the data model is timed as its own variant and
+    # pinned to the VALU one on the same problem
+    var = rec["variants"]
+    assert var["dofmap"]["dofmap_core"] == "valu" and var["dofmap_mfma"]["dofmap_core"] == "mfma"
+    assert rec["dofmap_mfma_gdofs"] > 0 and rec["q6_dofmap_mfma_gdofs"] > 0
+    for key in ("dofmap~dofmap_mfma", "q6_dofmap~q6_dofmap_mfma"):
+        pair = rec["consistency"]["pairs"][key]
+        assert pair["ok"] and pair["action_norm"] < 1e-12 and pair["action_wdot"] < 1e-12, pair
     bad = _bench(BDX_TEST_CORRUPT_DOFMAP="1")
     assert bad.returncode == 4, (bad.returncode, bad.stderr[-3000:])
     rec = _line(bad)  # the JSON line is still printed
