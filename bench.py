@@ -74,8 +74,9 @@ def parse_args(argv=None):
     ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
                     help="after the headline, time variants of it: the perturbed "
                          "(general trilinear) mesh, the "
-                         "reference's data model (dofmap + stored G, Q3 and Q6) and Q6 "
-                         "perturbed (GPU only; auto: on for one rank)")
+                         "reference's data model (dofmap + stored G, Q3 and Q6, on its VALU "
+                         "and its MFMA kernel), Q6 perturbed and Q6 FP32 perturbed (FP32 "
+                         "MFMA) (GPU only; auto: on for one rank)")
     ap.add_argument("--box-probe", default="on", choices=["on", "off"],
                     help="after every timed run, measure the box's HBM stream rate "
                          "(untimed context: config.box_stream)")
