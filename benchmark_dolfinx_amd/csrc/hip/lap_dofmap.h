@@ -60,6 +60,9 @@ enum { kDofAction = 0, kDofCG = 1 };
 // would expose the G latency at once: not used.
 constexpr bool kDofEarly = true;
 constexpr bool kDofGnt = true;
+// kDofZMerge: the Q3 instance scatters the z-lines of its two z-neighbour
+// cells as one 7-dof run (see the scatter at the end of the cell loop)
+constexpr bool kDofZMerge = true;
 typedef unsigned bdx_u32x2 __attribute__((ext_vector_type(2)));
 
 template <int NQ>
@@ -232,6 +235,9 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   constexpr int IB = 64 / CPW;               // iterations per id block
   constexpr int XPL = (24 + NQ2 - 1) / NQ2;  // vertex coordinates per lane (OTF)
   constexpr int NE = CPW * ND3, RE = (NE + 63) / 64;  // gathered elements / rounds per lane
+  // merged z-line scatter of the wave's two cells (see the scatter below)
+  // (FP64 only: the FP32 instance would drop from 3 to 2 waves / SIMD)
+  constexpr bool ZMERGE = kDofZMerge && CPW == 2 && ND == 4 && sizeof(T) == 8;
   const int first = c_beg + wv * CPW + slot;
   const int last_li = c_end - 1;
   const int wbase = c_beg + wv * CPW;  // list index of (iteration 0, slot 0)
@@ -704,12 +710,59 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     // wave-instruction carries ND-dof runs instead of one dof per lane (float
     // atomics execute as 64-B memory-side requests: MI355X_MICROARCH.md,
     // "Global float atomics")
+    if constexpr (ZMERGE) {
+      // two cells per wave with 4-dof z-lines (Q3): the wave's cells are
+      // consecutive in the launch list, i.e. z-neighbours on a lexicographic
+      // mesh, so each z-line of cell 0 ends at the dof where cell 1's begins.
+      // Where the scatter targets say so (per line, any mesh), the two lines
+      // are added as ONE 7-dof run with the shared dof summed first: 16 runs
+      // of 56 bytes per cell pair instead of 32 runs of 32 bytes, i.e. fewer
+      // 64-byte memory-side atomic requests (and one atomic per shared dof).
+      // Lines that do not meet take the spare lanes 112..127 for cell 1's
+      // first dof.
+      int* const tg = reinterpret_cast<int*>(s_buf[wv][0][1]);  // Bb: free since the last sync
 #pragma unroll
-    for (int r = 0; r < RE; ++r) {
-      if (lane + 64 * r < NE && dsc[r] >= 0) {
-        const T v = s_buf[wv][e_slot(r)][2][e_loc(r)];
-        if constexpr (MODE == kDofCG) pap += static_cast<double>(ue[r]) * static_cast<double>(v);
-        atomicAdd(A.y + dsc[r], v);
+      for (int r = 0; r < RE; ++r) {
+        const T v = s_buf[wv][r][2][lane];
+        if constexpr (MODE == kDofCG) {
+          if (dsc[r] >= 0) pap += static_cast<double>(ue[r]) * static_cast<double>(v);
+        }
+        tg[64 * r + lane] = dsc[r];
+      }
+      dof_wave_sync();
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int q = lane + 64 * r;
+        int t;
+        T v;
+        if (q < 112) {
+          const int l = q / 7, m = q - (q / 7) * 7;  // line, position in the 7-dof run
+          if (m < 3) {
+            t = tg[l * 4 + m];
+            v = s_buf[wv][0][2][l * 4 + m];
+          } else if (m == 3) {  // the shared dof: cell 1's part joins when the lines meet
+            t = tg[l * 4 + 3];
+            const bool meet = t == tg[64 + l * 4];
+            v = s_buf[wv][0][2][l * 4 + 3] + (meet ? s_buf[wv][1][2][l * 4] : T(0));
+          } else {
+            t = tg[64 + l * 4 + m - 3];
+            v = s_buf[wv][1][2][l * 4 + m - 3];
+          }
+        } else {
+          const int l = q - 112;  // cell 1's first dof of line l when the lines do not meet
+          t = tg[l * 4 + 3] == tg[64 + l * 4] ? -1 : tg[64 + l * 4];
+          v = s_buf[wv][1][2][l * 4];
+        }
+        if (t >= 0) atomicAdd(A.y + t, v);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RE; ++r) {
+        if (lane + 64 * r < NE && dsc[r] >= 0) {
+          const T v = s_buf[wv][e_slot(r)][2][e_loc(r)];
+          if constexpr (MODE == kDofCG) pap += static_cast<double>(ue[r]) * static_cast<double>(v);
+          atomicAdd(A.y + dsc[r], v);
+        }
       }
     }
     dof_wave_sync();  // the next cell reuses the wave's buffers
