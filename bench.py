@@ -568,7 +568,8 @@ def _stream_probe(comm, n: int, reps: int = 10) -> dict:
     2 reads + 1 write, the CG update pass's access pattern.  Boxes of this pool
     differ by 7-12 % on the stream-bound configs (Q3, the dofmap data model)
     while the compute-side Q6 ones do not (profiles/r5_final_repeat.md); this
-    puts the box's rate next to the number.  TB/s, min / max over ranks."""
+    puts the box's rate next to the number.  TB/s, min / max over ranks; and
+    the box's DGEMM rate (TFLOP/s) as its compute-side counterpart."""
     import torch
     r = torch.ones(n, dtype=torch.float64, device="cuda")
     y = torch.ones_like(r)
@@ -582,10 +583,26 @@ def _stream_probe(comm, n: int, reps: int = 10) -> dict:
     torch.cuda.synchronize()
     tbps = 24.0 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12
     del r, y
+    # the box's FP64 compute rate next to it: a 4096^3 DGEMM (rocBLAS), the
+    # side that the compute-heavy configs (Q6, perturbed) lean on
+    m = 4096
+    a_ = torch.rand(m, m, dtype=torch.float64, device="cuda")
+    b_ = torch.rand(m, m, dtype=torch.float64, device="cuda")
+    c_ = a_ @ b_
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        torch.mm(a_, b_, out=c_)
+    e1.record()
+    torch.cuda.synchronize()
+    tflops = 2.0 * m ** 3 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    del a_, b_, c_
     torch.cuda.empty_cache()
     return {"op": "r += a*y, fp64, 2R1W", "n": n,
             "tbps_min": -comm.allreduce_scalar(-tbps, "max"),
-            "tbps_max": comm.allreduce_scalar(tbps, "max")}
+            "tbps_max": comm.allreduce_scalar(tbps, "max"),
+            "dgemm_tflops_min": -comm.allreduce_scalar(-tflops, "max"),
+            "dgemm_tflops_max": comm.allreduce_scalar(tflops, "max")}
 
 
 def _record(a, n, head, companions, extras, flags, gpu) -> dict:

@@ -36,6 +36,7 @@ def test_bench_run_multirank_matches_single(config, total, ranks):
     assert got["config"]["mesh"] == ref["config"]["mesh"]
     bs = got["config"]["box_stream"]  # the untimed box probe, reduced over ranks
     assert bs["n"] > 0 and 0 < bs["tbps_min"] <= bs["tbps_max"]
+    assert 0 < bs["dgemm_tflops_min"] <= bs["dgemm_tflops_max"]
     tol = 1e-11 if config != "q6f32" else 2e-5
     assert abs(got["config"]["y_norm"] - ref["config"]["y_norm"]) <= tol * ref["config"]["y_norm"]
     if config == "q3":
