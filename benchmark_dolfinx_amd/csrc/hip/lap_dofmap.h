@@ -63,6 +63,11 @@ constexpr bool kDofGnt = true;
 // kDofZMerge: the Q3 instance scatters the z-lines of its two z-neighbour
 // cells as one 7-dof run (see the scatter at the end of the cell loop)
 constexpr bool kDofZMerge = true;
+// kDofWgMerge: the one-cell-per-wave instances (NQ >= 8) and the FP64 Q3 one
+// (two cells per wave) scatter the z-lines of the workgroup's cells of an
+// iteration (consecutive in the launch list: z-neighbours on a lexicographic
+// mesh) as one run per line, after a workgroup barrier
+constexpr bool kDofWgMerge = true;
 typedef unsigned bdx_u32x2 __attribute__((ext_vector_type(2)));
 
 template <int NQ>
@@ -238,6 +243,8 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
   // merged z-line scatter of the wave's two cells (see the scatter below)
   // (FP64 only: the FP32 instance would drop from 3 to 2 waves / SIMD)
   constexpr bool ZMERGE = kDofZMerge && CPW == 2 && ND == 4 && sizeof(T) == 8;
+  // workgroup-merged scatter of the waves' cells (supersedes ZMERGE)
+  constexpr bool WGMERGE = kDofWgMerge && (CPW == 1 || ZMERGE) && ND3 <= 512;
   const int first = c_beg + wv * CPW + slot;
   const int last_li = c_end - 1;
   const int wbase = c_beg + wv * CPW;  // list index of (iteration 0, slot 0)
@@ -326,8 +333,10 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     }
   };
 
-  const bool wave_on = wbase < c_end;
-  const int nit = wave_on ? (c_end - wbase + STEP - 1) / STEP : 0;  // iterations of this wave
+  // WGMERGE: every wave of the block runs the block's iteration count (the
+  // scatter has workgroup barriers); a wave past the end runs masked cells
+  const bool wave_on = WGMERGE ? c_beg < c_end : wbase < c_end;
+  const int nit = !wave_on ? 0 : (c_end - (WGMERGE ? c_beg : wbase) + STEP - 1) / STEP;
   int dA[RE], dB[RE], vA[XPL], vB[XPL];
   int cell_cur = 0, id_next = 0;
   Gather gc;
@@ -710,7 +719,7 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
     // wave-instruction carries ND-dof runs instead of one dof per lane (float
     // atomics execute as 64-B memory-side requests: MI355X_MICROARCH.md,
     // "Global float atomics")
-    if constexpr (ZMERGE) {
+    if constexpr (ZMERGE && !WGMERGE) {
       // two cells per wave with 4-dof z-lines (Q3): the wave's cells are
       // consecutive in the launch list, i.e. z-neighbours on a lexicographic
       // mesh, so each z-line of cell 0 ends at the dof where cell 1's begins.
@@ -755,6 +764,66 @@ __global__ void __launch_bounds__(DofShape<NQ>::NT)
         }
         if (t >= 0) atomicAdd(A.y + t, v);
       }
+    } else if constexpr (WGMERGE) {
+      // the workgroup's cells of this iteration are consecutive in the launch
+      // list (wave w, slot s: list entry c_beg + CPW w + s + STEP j), i.e. a
+      // z-run of cells on a lexicographic mesh: every z-line goes out as one
+      // run through them, each junction's shared dof summed first when the
+      // scatter targets say the lines meet (per line and junction, so any
+      // mesh stays correct; a junction that does not meet gives the next
+      // cell's first dof to an extra entry).  One run of NC (ND - 1) + 1 dofs
+      // per line instead of NC runs of ND: fewer 64-byte memory-side atomic
+      // requests, one atomic per shared dof.
+      int* const tg = reinterpret_cast<int*>(s_buf[wv][0][1]);  // Bb: free since the last sync
+#pragma unroll
+      for (int r = 0; r < RE; ++r) {
+        if (lane + 64 * r < NE) {
+          if constexpr (MODE == kDofCG) {
+            if (dsc[r] >= 0)
+              pap += static_cast<double>(ue[r]) *
+                     static_cast<double>(s_buf[wv][e_slot(r)][2][e_loc(r)]);
+          }
+          tg[lane + 64 * r] = dsc[r];  // slot s's entries at s ND^3
+        }
+      }
+      __syncthreads();
+      constexpr int W4 = S::WAVES * CPW, RL = W4 * (ND - 1) + 1, NXL = W4 - 1;  // run / extras per line
+      constexpr int NLN = ND * ND, NB = NLN * (RL + NXL);
+      // cell c of the iteration: wave c / CPW, slot c % CPW
+      auto tgt = [&](int c, int e) {
+        return reinterpret_cast<const int*>(s_buf[c / CPW][0][1])[(c % CPW) * ND3 + e];
+      };
+      auto val = [&](int c, int e) { return s_buf[c / CPW][c % CPW][2][e]; };
+#pragma unroll 1
+      for (int q = tid; q < NB; q += S::NT) {
+        int t;
+        T v;
+        if (q < NLN * RL) {
+          const int l = q / RL, m = q - (q / RL) * RL;
+          // position m of the run: cell w = m / (ND - 1), its dof k = m % (ND - 1),
+          // except the last cell's last dof (m = RL - 1)
+          const int w = m < RL - 1 ? m / (ND - 1) : W4 - 1;
+          const int k = m < RL - 1 ? m - w * (ND - 1) : ND - 1;
+          t = tgt(w, l * ND + k);
+          v = val(w, l * ND + k);
+          if (k == 0 && w > 0) {
+            // a junction: this entry carries the previous cell's last dof
+            // (summed with ours when they meet); ours alone goes out as an
+            // extra entry otherwise
+            const int tp = tgt(w - 1, l * ND + ND - 1);
+            const T vp = val(w - 1, l * ND + ND - 1);
+            v = tp == t ? vp + v : vp;
+            t = tp;
+          }
+        } else {
+          const int q2 = q - NLN * RL, l = q2 / NXL, w = q2 - (q2 / NXL) * NXL + 1;
+          const int tn = tgt(w, l * ND);  // cell w's first dof when the junction does not meet
+          t = tgt(w - 1, l * ND + ND - 1) == tn ? -1 : tn;
+          v = val(w, l * ND);
+        }
+        if (t >= 0) atomicAdd(A.y + t, v);
+      }
+      __syncthreads();  // every wave's buffers are read before the next cell reuses them
     } else {
 #pragma unroll
       for (int r = 0; r < RE; ++r) {
