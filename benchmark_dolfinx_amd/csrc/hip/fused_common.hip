@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(256)
         if (zq * sz > k) --zq;
         if ((zq + 1) * sz <= k) ++zq;
         if (zq * sz == k && zq >= 1 && zq < ntz) {
-          t += zb[(i * L1 + j) * (ntz - 1) + zq - 1];
+          t += zb[(i * (ntz - 1) + zq - 1) * L1 + j];
           if (yrow >= 0) t += cb[(i * (nty - 1) + yrow) * (ntz - 1) + zq - 1];
         }
         const T rn = vr[u][e] - alpha * t;
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(256)
             if (w < nw) t[w] += yr[w];
         }
         if (lz0 == 0 && tZ >= 1 && tZ < ntz) {
-          t[0] += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
+          t[0] += zb[(x * (ntz - 1) + tZ - 1) * L1 + gy];
           if (yrow >= 0) t[0] += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
         }
 #pragma unroll
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(256)
           T t = vy[w];
           if (yrow >= 0) t += yb[(x * (nty - 1) + yrow) * Lz + gz];
           if (lz == 0 && tZ >= 1 && tZ < ntz) {
-            t += zb[(x * L1 + gy) * (ntz - 1) + tZ - 1];
+            t += zb[(x * (ntz - 1) + tZ - 1) * L1 + gy];
             if (yrow >= 0) t += cb[(x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1];
           }
           const T rn = vr[w] - alpha * t;
@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(256)
           for (int w = 0; w < W; ++w) ia[u][w] = ldb(rs_yb, bo(yneed && gz0 + w < o2, ye + w));
         }
         const bool z0 = row && gz0 < o2 && lz0 == 0 && zt;
-        ia[u][W] = ldb(rs_zb, bo(z0, (x * L1 + gy) * (ntz - 1) + tZ - 1));
+        ia[u][W] = ldb(rs_zb, bo(z0, (x * (ntz - 1) + tZ - 1) * L1 + gy));
         ia[u][W + 1] = ldb(rs_cb, bo(z0 && yrow >= 0, (x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1));
       } else {
         int lz = ein - ly * tsz - 1;
@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(256)
           const int yrow = (ly == 0 && tY >= 1 && tY < nty) ? tY - 1 : -1;
           const bool zf = on && lz == 0 && zt;
           ia[u][3 * w] = ldb(rs_yb, bo(on && yrow >= 0, (x * (nty - 1) + yrow) * Lz + gz));
-          ia[u][3 * w + 1] = ldb(rs_zb, bo(zf, (x * L1 + gy) * (ntz - 1) + tZ - 1));
+          ia[u][3 * w + 1] = ldb(rs_zb, bo(zf, (x * (ntz - 1) + tZ - 1) * L1 + gy));
           ia[u][3 * w + 2] = ldb(rs_cb, bo(zf && yrow >= 0, (x * (nty - 1) + yrow) * (ntz - 1) + tZ - 1));
         }
       }

@@ -166,7 +166,7 @@ struct FusedArgs {
   T* __restrict__ pnew;         // CG: new p (written, tile-owned dofs)
   T* __restrict__ y;            // output (tile-owned dofs)
   T* __restrict__ yb;           // [Lx][nty-1][Lz]   upper-y face partials
-  T* __restrict__ zb;           // [Lx][Ly][ntz-1]   upper-z face partials
+  T* __restrict__ zb;           // [Lx][ntz-1][Ly]   upper-z face partials (a tile face contiguous)
   T* __restrict__ cb;           // [Lx][nty-1][ntz-1] upper corner partials
   const T* __restrict__ G;      // stored geometry (GEOM=stored)
   const T* __restrict__ xv;     // vertex coordinates (GEOM=otf)
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads), Fuse
       } else if (!iy && iz) {
         A.yb[(gx * (A.nty - 1) + ty) * Lz + gz] = v;
       } else if (iy && !iz) {
-        A.zb[(gx * Ly + gy) * (A.ntz - 1) + tz] = v;
+        A.zb[(gx * (A.ntz - 1) + tz) * Ly + gy] = v;
       } else {
         A.cb[(gx * (A.nty - 1) + ty) * (A.ntz - 1) + tz] = v;
       }
@@ -687,15 +687,15 @@ __global__ void __launch_bounds__(256)
       T add = yb[t];
       const int64_t tzz = z / sz;
       if (z % sz == 0 && tzz >= 1 && tzz < ntz) {
-        add += zb[(x * Ly + yy) * (ntz - 1) + (tzz - 1)];
+        add += zb[(x * (ntz - 1) + (tzz - 1)) * Ly + yy];
         add += cb[(x * (nty - 1) + tym1) * (ntz - 1) + (tzz - 1)];
       }
       y[lat.sidx(x, yy, z)] += add;
     } else {
       const int64_t s = t - n1;
-      const int64_t tzm1 = s % (ntz - 1);
-      const int64_t r = s / (ntz - 1);
-      const int64_t yy = r % Ly, x = r / Ly;
+      const int64_t yy = s % Ly;
+      const int64_t r = s / Ly;
+      const int64_t tzm1 = r % (ntz - 1), x = r / (ntz - 1);
       const int64_t tyy = yy / sy;
       if (yy % sy == 0 && tyy >= 1 && tyy < nty) continue;  // handled by the YB pass
       const int64_t z = (tzm1 + 1) * sz;
@@ -733,20 +733,20 @@ __global__ void __launch_bounds__(256)
       T add = yb[(x * (nty - 1) + tym1) * Lz + z];
       const int64_t tzz = z / sz;
       if (z % sz == 0 && tzz >= 1 && tzz < ntz) {
-        add += zb[(x * Ly + yy) * (ntz - 1) + (tzz - 1)];
+        add += zb[(x * (ntz - 1) + (tzz - 1)) * Ly + yy];
         add += cb[(x * (nty - 1) + tym1) * (ntz - 1) + (tzz - 1)];
       }
       y[lat.sidx(x, yy, z)] += add;
     } else if (t < nA1 + nA2) {  // ZB column entry on the x ghost plane
       const int64_t s = t - nA1, x = Lx - 1;
-      const int64_t tzm1 = s % (ntz - 1), yy = s / (ntz - 1);
+      const int64_t yy = s % Ly, tzm1 = s / Ly;
       const int64_t tyy = yy / sy;
       if (yy % sy == 0 && tyy >= 1 && tyy < nty) continue;  // on a YB row: done above
-      y[lat.sidx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
+      y[lat.sidx(x, yy, (tzm1 + 1) * sz)] += zb[(x * (ntz - 1) + tzm1) * Ly + yy];
     } else if (t < nA1 + nA2 + nB) {  // ZB column entry on the y ghost plane
       const int64_t s = t - nA1 - nA2, yy = Ly - 1;
       const int64_t tzm1 = s % (ntz - 1), x = s / (ntz - 1);
-      y[lat.sidx(x, yy, (tzm1 + 1) * sz)] += zb[(x * Ly + yy) * (ntz - 1) + tzm1];
+      y[lat.sidx(x, yy, (tzm1 + 1) * sz)] += zb[(x * (ntz - 1) + tzm1) * Ly + yy];
     } else {  // YB row entry on the z ghost plane
       const int64_t s = t - nA1 - nA2 - nB, z = Lz - 1;
       const int64_t tym1 = s % (nty - 1), x = s / (nty - 1);

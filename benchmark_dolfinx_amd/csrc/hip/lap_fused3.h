@@ -325,7 +325,7 @@ __global__ void __launch_bounds__((FusedShape<T, ND, NQ, TY, TZ>::threads),
           off = static_cast<int>(pl * A.ybps) + ty * Lz + gz;
         } else if (iy && !iz) {
           kind = 2;
-          off = static_cast<int>(pl * A.zbps) + gy * (A.ntz - 1) + tz;
+          off = static_cast<int>(pl * A.zbps) + tz * Ly + gy;
         } else {
           kind = 3;
           off = static_cast<int>(pl * A.cbps) + ty * (A.ntz - 1) + tz;
